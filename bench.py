@@ -1,0 +1,326 @@
+#!/usr/bin/env python3
+"""Benchmark of the SrcDsp hot path on MI355X (driver contract: one JSON line).
+
+Default workload = BASELINE.json configs[1] (the headline metric): the 127-tap
+complex<float> decimate-by-4 FilterDnsamplingFir over 2^28 device-resident
+synthetic samples, one step() per timed step (one kernel launch), FMA float
+contract.  With --gpus N (launched by torch.distributed.run) every rank owns
+its own channel(s) -- configs[2]'s channel sharding, weak scaling, no
+collective in the timed region; the RCCL result gather to rank 0 is timed
+separately (gather_ms).
+
+Other workloads (--workload): mixdecim (config 4, mixer -> fixed-point
+decimator, fused), corr (config 5, 1024-lag correlator), fir (config 1 shape on
+the GPU).
+
+Reported beside the GPU number:
+  roofline      dominant kernel's algorithmic bytes / its HIP-event time, vs 8 TB/s
+  cpu_baseline  the REFERENCE (oracle/_ref, g++ -O2) timed on this host, 1 thread
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Msamples/sec (in) for 127-tap cplx<float> decim-4 polyphase FIR, 256 Msamp; %HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+SEED = 0x5EED
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--workload", default="decim", choices=["decim", "mixdecim", "corr", "fir"])
+    p.add_argument("--samples", type=int, default=1 << 28, help="input samples per channel per step")
+    p.add_argument("--channels-per-gpu", type=int, default=1)
+    p.add_argument("--fp", default="fma", choices=["fma", "strict"])
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-sample", type=int, default=1 << 27, help="samples timed on the reference CPU path")
+    p.add_argument("--no-gather", action="store_true")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return p.parse_args()
+
+
+def dist_setup(args):
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def barrier(world):
+    import torch
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(x, world):
+    import torch
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+# ---------------------------------------------------------------- workloads
+class Workload:
+    """One step = one pass of the hot path over one batch of resident input."""
+    name = ""
+    bytes_per_sample = 0.0   # algorithmic HBM bytes per input sample
+    dtype = ""
+
+    def step(self):
+        raise NotImplementedError
+
+
+class DecimWorkload(Workload):
+    dtype = "f32"
+    bytes_per_sample = 10.0  # 8 B complex<float> read + 8 B out per 4 inputs
+
+    def __init__(self, S, torch, L, channels, rank, fp):
+        from srcdsp_amd.design import hamming_sinc
+        self.c = hamming_sinc(127)
+        self.L, self.C = L, channels
+        self.x = torch.empty((channels, L), dtype=torch.complex64, device="cuda")
+        for ch in range(channels):
+            S.fill_synthetic(self.x[ch], "cf32", seed=SEED, channel=rank * channels + ch)
+        self.y = torch.empty((channels, L // 4), dtype=torch.complex64, device="cuda")
+        self.f = [S.FilterDnsamplingFir(self.c, 4, fp=fp) for _ in range(channels)]
+        self.S = S
+        self.name = "decim_cf32_m4_t127"
+
+    def step(self):
+        if self.C == 1:
+            self.f[0].step(self.x[0], self.y[0])
+        else:
+            self.S.decim_step_batched(self.f, self.x, self.y)
+
+
+class MixDecimWorkload(Workload):
+    dtype = "i32"
+    bytes_per_sample = 5.0  # 4 B complex<int16_t> read + 4 B out per 4 inputs
+
+    def __init__(self, S, torch, L, channels, rank, fp):
+        from srcdsp_amd.design import hamming_sinc, q14
+        cq = q14(hamming_sinc(127))
+        self.x = torch.empty((L, 2), dtype=torch.int16, device="cuda")
+        S.fill_synthetic(self.x, "ci16", seed=SEED, channel=rank, lo=-8192, hi=8191)
+        self.y = torch.empty((L // 4, 2), dtype=torch.int16, device="cuda")
+        m = S.Mixer(4096)
+        m.reset(0.1)
+        d = S.FilterDnsamplingFir(cq, 4, "complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int32_t")
+        self.chain = S.MixerDecimatorChain(m, d)
+        self.name = "mixer4096_f0.1_to_decim_ci16_q14_m4_t127"
+
+    def step(self):
+        self.chain.step(self.x, self.y)
+
+
+class CorrWorkload(Workload):
+    dtype = "i32"
+    bytes_per_sample = 4.0
+
+    def __init__(self, S, torch, L, channels, rank, fp):
+        from srcdsp_amd.design import qpsk_pattern
+        self.p = qpsk_pattern(1024, 500, seed=2)
+        rng = np.random.default_rng(rank)
+        x = rng.integers(-125, 126, size=(L, 2)).astype(np.int32)
+        off = (3 * L) // 4
+        x[off:off + 1024] += 2 * self.p
+        self.x = torch.from_numpy(np.clip(x, -32768, 32767).astype(np.int16)).cuda()
+        self.S = S
+        self.name = "corr_1024x1"
+        self.expect = off + 1023 - 1
+
+    def step(self):
+        g = self.S.FixedPatternCorrelator(1024, 1)
+        g.setPattern(self.p)
+        found, idx = g.step(self.x)
+        self.last = (found, idx)
+
+
+class FirWorkload(Workload):
+    dtype = "f32"
+    bytes_per_sample = 12.0  # 4 B float in, 8 B complex<float> out
+
+    def __init__(self, S, torch, L, channels, rank, fp):
+        from srcdsp_amd.design import hamming_sinc
+        self.x = torch.randint(-2048, 2048, (L,), device="cuda").float()
+        self.y = torch.empty(L, dtype=torch.complex64, device="cuda")
+        self.f = S.FilterFir(hamming_sinc(31, 0.2), "float", "complex<float>", "float", "float", fp=fp)
+        self.name = "fir_f32_t31"
+
+    def step(self):
+        self.f.step(self.x, self.y)
+
+
+WORKLOADS = {"decim": DecimWorkload, "mixdecim": MixDecimWorkload, "corr": CorrWorkload, "fir": FirWorkload}
+
+
+# ---------------------------------------------------------------- CPU baseline
+def cpu_baseline(args):
+    """Time the reference itself (oracle/_ref/strict, g++ -O2, 1 thread) on a
+    bounded sample of the same workload; test infrastructure, never the product."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    from srcdsp_amd.design import hamming_sinc
+    if args.workload != "decim":
+        return None
+    d = os.path.join(ROOT, "oracle", "_ref", "strict")
+    path = os.path.join(d, "libref_decim_old.so")
+    n = min(args.cpu_sample, args.samples)
+    n -= n % 4
+    if os.path.exists(path):
+        lib = C.CDLL(path)
+        lib.ref_decim_create.restype = C.c_void_p
+        lib.ref_decim_create.argtypes = [C.c_int, C.c_uint, C.c_void_p, C.c_int]
+        lib.ref_decim_step_timed.restype = C.c_double
+        lib.ref_decim_step_timed.argtypes = [C.c_void_p, C.c_void_p, C.c_long, C.c_void_p]
+        lib.ref_decim_destroy.argtypes = [C.c_void_p]
+        c = hamming_sinc(127)
+        h = lib.ref_decim_create(0, 4, c.ctypes.data, 127)
+        x = pyoracle.Oracle(0).gen_cf32(SEED, 0, 0, n)
+        y = np.zeros(n // 4, np.complex64)
+        secs = lib.ref_decim_step_timed(h, x.ctypes.data, n, y.ctypes.data)
+        lib.ref_decim_destroy(h)
+        kind = "reference"
+        src = "oracle/_ref/strict/libref_decim_old.so (dnsampling_filters.h built g++ -O2, x86-64 baseline)"
+    else:  # no reference build travelled: time the C restatement instead
+        o = pyoracle.Oracle(0)
+        x = o.gen_cf32(SEED, 0, 0, n)
+        f = o.decim(0, 4, hamming_sinc(127))
+        t0 = time.perf_counter()
+        f.step(x)
+        secs = time.perf_counter() - t0
+        kind = "port"
+        src = "oracle/liboracle.so (C restatement, -O2)"
+    cpu = ""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            cpu = next(l.split(":", 1)[1].strip() for l in fh if l.startswith("model name"))
+    except Exception:
+        pass
+    return {"value": round(n / secs / 1e6, 3), "unit": "Msamples/s", "cores": 1, "kind": kind,
+            "sample": f"{n} samples (first {n} of channel 0 of the same synthetic workload), one step() call, "
+                      f"{secs:.2f} s; {src}; host CPU: {cpu}"}
+
+
+def pmc_traffic(args, work_name, per_launch_samples):
+    """Per-launch HBM bytes from the committed rocprofv3 PMC summary (see
+    profiles/README.md for how it is collected and corrected), if it matches."""
+    try:
+        with open(args.traffic_json) as f:
+            t = json.load(f)
+        e = t.get(work_name)
+        if e and int(e.get("samples_per_launch", -1)) == per_launch_samples:
+            return e.get("hbm_bytes_per_launch")
+    except Exception:
+        pass
+    return None
+
+
+# ---------------------------------------------------------------- main
+def main():
+    args = parse()
+    import torch
+    world, rank, local = dist_setup(args)
+    import srcdsp_amd as S
+    S.lib()  # loud failure if the HIP library is missing
+    L = args.samples - args.samples % 4
+    work = WORKLOADS[args.workload](S, torch, L, args.channels_per_gpu, rank, args.fp)
+    stream = torch.cuda.current_stream()
+
+    for _ in range(args.warmup):
+        work.step()
+    barrier(world)
+
+    # timed region: K steps, barrier + synchronize on both sides
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    barrier(world)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        work.step()
+        ev[i][1].record(stream)
+    barrier(world)
+    t1 = time.perf_counter()
+    wall = max_over_ranks(t1 - t0, world)
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    kern_avg_ms = float(np.mean(kern_ms))
+
+    units_per_rank = L * (args.channels_per_gpu if args.workload == "decim" else 1) * args.steps
+    total_samples = units_per_rank * world
+    value = total_samples / wall / 1e6
+    ms_per_step = wall / args.steps * 1e3
+
+    gather_ms = None
+    if world > 1 and not args.no_gather and args.workload == "decim":
+        # configs[2]: gather every rank's decimated channels to rank 0 over RCCL (xGMI)
+        import torch.distributed as dist
+        y = work.y
+        bufs = [torch.empty_like(y) for _ in range(world)] if rank == 0 else None
+        barrier(world)
+        g0 = time.perf_counter()
+        dist.gather(y, bufs, dst=0)
+        barrier(world)
+        gather_ms = (time.perf_counter() - g0) * 1e3
+        del bufs
+
+    per_launch_samples = L * args.channels_per_gpu if args.workload == "decim" else L
+    achieved = work.bytes_per_sample * per_launch_samples / (kern_avg_ms * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args, work.name, per_launch_samples),
+            "kernel": work.name, "kernel_ms": round(kern_avg_ms, 4),
+            "algorithmic_bytes_per_launch": int(work.bytes_per_sample * per_launch_samples)}
+    if args.workload == "corr":
+        roof["bound"] = "valu"
+        roof["note"] = "integer-MAC bound (2048 MAC/sample), GB/s shown for reference only"
+
+    if rank == 0:
+        cfg = {"workload": work.name, "samples_per_channel": L, "channels_per_gpu": args.channels_per_gpu,
+               "taps": 127 if args.workload in ("decim", "mixdecim") else None, "decimation": 4,
+               "fp_contract": args.fp, "parallelism": f"channels sharded over {world} GPU(s)",
+               "timed": "device-resident input, one step() per step; PCIe excluded"}
+        line = {"metric": METRIC if args.workload == "decim" else f"Msamples/sec (in), {work.name}",
+                "value": round(value, 2), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": work.dtype,
+                "data": "synthetic (counter-based splitmix64 integer samples, SURVEY §8d)", "config": cfg,
+                "roofline": roof}
+        if gather_ms is not None:
+            line["gather_ms"] = round(gather_ms, 3)
+            line["gather_bytes"] = int(world * work.y.numel() * work.y.element_size())
+        if args.workload == "corr":
+            line["detection"] = list(work.last)
+        if not args.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline(args)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

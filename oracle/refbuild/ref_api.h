@@ -29,6 +29,7 @@ void ref_decim_set_left_shift(void *h, int ls);
 void ref_decim_reset(void *h);
 void ref_decim_step(void *h, const void *in, long n_in, void *out);
 void ref_decim_destroy(void *h);
+double ref_decim_step_timed(void *h, const void *in, long n_in, void *out);
 
 /* dsptl_dnsampling_filters.h (current header; setCoeffs asserts N%M==0) */
 void *ref_decim2_create(int variant, unsigned M, const void *coeffs, int ntaps);

@@ -21,4 +21,9 @@ void ref_decim_step(void *h, const void *in, long n_in, void *out) {
     static_cast<DecimBase *>(h)->step(in, n_in, out);
 }
 void ref_decim_destroy(void *h) { delete static_cast<DecimBase *>(h); }
+/* step() timed around the reference call alone (excludes the harness copies);
+ * used by bench.py's cpu_baseline leg */
+double ref_decim_step_timed(void *h, const void *in, long n_in, void *out) {
+    return static_cast<DecimBase *>(h)->stepTimed(in, n_in, out);
+}
 }

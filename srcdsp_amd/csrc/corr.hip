@@ -1,0 +1,381 @@
+// corr.hip -- dsptl::FixedPatternCorrelator<int16_t, int32_t, N, S>
+// (correlators.h:54-316) on gfx950.
+//
+// The reference walks the input one sample at a time and stops at the first
+// detection.  Everything it computes per sample depends only on the window of
+// N*S samples ending there, so the step is split into
+//   1. corr_eval   : every sample's scaled correlation |C_i>>2|^2 and scaled
+//                    window energy, in parallel (int32 wrap-around arithmetic
+//                    as the reference's complex<int32_t>/uint32 registers);
+//   2. corr_detect : the 3-point peak + threshold test of correlators.h:262-268
+//                    on each index, reduced to the FIRST index with atomicMin;
+//   3. host        : state update -- the registers, the N*S-1 sample history
+//                    (the detected sample is dropped: the reference `break`s
+//                    without advancing `top`, correlators.h:291), bitSamples.
+// The double-precision threshold sqrt(c) > sqrt(e)*2.7 is evaluated exactly:
+// sqrt(e) > 300 <=> e > 90000 for integer e, and the correctly rounded sqrt of
+// a uint32 is obtained from the hardware estimate by an exact 128-bit
+// neighbour check, so no tolerance is involved.
+#include <algorithm>
+#include <vector>
+
+#include "ops.h"
+
+namespace srcdsp {
+
+struct srcdsp_corr_state {
+    unsigned N = 0, S = 1, NS = 0;
+    int32_t *d_coef = nullptr;   // conj(pattern), N complex<int32_t> (2N int32)
+    std::vector<int32_t> h_coef;
+    uint32_t *d_hist[2] = {nullptr, nullptr};  // last NS-1 effective samples (packed ci16)
+    int cur = 0;
+    uint32_t *d_corr = nullptr, *d_en = nullptr;  // per-sample scratch
+    size_t scratch_cap = 0;
+    unsigned *d_best = nullptr;
+    // CorrState (correlators.h:59-81)
+    uint32_t energy[3] = {0, 0, 0}, corr[3] = {0, 0, 0};
+    uint32_t coeffs_energy = 0;
+    int coeff_scaling = 0;
+    double threshold_factor = 0;
+    std::vector<int16_t> bits;  // bitSamples, N complex<int16_t>
+    Ordering order;
+    HostStage stage;
+};
+
+// ------------------------------------------------ exact double sqrt of uint32
+__device__ __forceinline__ bool rn_sqrt_ok(double s, uint32_t n) {
+    // s = m * 2^q is RN(sqrt(n)) iff (2m-1)^2 < n * 2^(2-2q) < (2m+1)^2 (no ties
+    // for integer n), checked in exact 128-bit integer arithmetic.
+    if (s <= 0) return n == 0 && s == 0;
+    unsigned long long b = (unsigned long long)__double_as_longlong(s);
+    int E = (int)((b >> 52) & 0x7ff);
+    unsigned long long m = (b & ((1ull << 52) - 1)) | (1ull << 52);
+    int K = -2 * (E - 1075) + 2;  // n * 2^K
+    if (K < 0 || K > 127 - 32) return false;
+    unsigned __int128 T = (unsigned __int128)n << K;
+    unsigned __int128 lo = (unsigned __int128)(2 * m - 1) * (2 * m - 1);
+    unsigned __int128 hi = (unsigned __int128)(2 * m + 1) * (2 * m + 1);
+    return lo < T && T < hi;
+}
+
+// neighbouring doubles of a positive finite value
+__device__ __forceinline__ double dnext(double s, long long d) {
+    return __longlong_as_double(__double_as_longlong(s) + d);
+}
+
+__device__ double crsqrt_u32(uint32_t n) {
+    if (n == 0) return 0.0;
+    const double s = __builtin_sqrt((double)n);
+    if (rn_sqrt_ok(s, n)) return s;
+    for (long long d = 1; d <= 4; ++d) {
+        if (rn_sqrt_ok(dnext(s, -d), n)) return dnext(s, -d);
+        if (rn_sqrt_ok(dnext(s, d), n)) return dnext(s, d);
+    }
+    return s;  // unreachable: the hardware estimate is within a few ulp
+}
+
+// correlators.h:262-268 evaluated exactly
+__device__ __forceinline__ bool corr_hit(uint32_t c2, uint32_t c1, uint32_t c0, uint32_t e1) {
+    if (!(c1 > c2 && c1 > c0)) return false;
+    if (e1 <= 90000u) return false;  // sqrt(e) > 300 in double <=> e >= 90001
+    const double cm = crsqrt_u32(c1), em = crsqrt_u32(e1);
+    return cm > em * 2.7;
+}
+
+// ------------------------------------------------------------------ kernels
+__device__ __forceinline__ uint32_t corr_fetch(const uint32_t *in, const uint32_t *hist, long j, long NSm1) {
+    return j >= 0 ? in[j] : (j + NSm1 >= 0 ? hist[j + NSm1] : 0u);
+}
+
+constexpr int kCorrBlock = 256;
+
+// one output per lane; the block's window span and the taps are staged in LDS
+__global__ __launch_bounds__(kCorrBlock) void corr_eval(const uint32_t *__restrict__ in, long n,
+                                                        const uint32_t *__restrict__ hist,
+                                                        const int32_t *__restrict__ coef, unsigned N, unsigned S,
+                                                        unsigned cs, uint32_t *__restrict__ corr_out,
+                                                        uint32_t *__restrict__ en_out) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+    const long NSm1 = (long)N * S - 1;
+    const long span = kCorrBlock + NSm1;  // samples i0-NSm1 .. i0+255
+    uint32_t *xs = sm;
+    int2 *cs2 = (int2 *)(sm + ((span + 3) & ~3l));
+    const long i0 = (long)blockIdx.x * kCorrBlock;
+    for (long k = threadIdx.x; k < span; k += kCorrBlock) {
+        long j = i0 - NSm1 + k;
+        xs[k] = j < n ? corr_fetch(in, hist, j, NSm1) : 0u;
+    }
+    for (unsigned m = threadIdx.x; m < N; m += kCorrBlock) cs2[m] = make_int2(coef[2 * m], coef[2 * m + 1]);
+    __syncthreads();
+    const long i = i0 + threadIdx.x;
+    if (i >= n) return;
+    uint32_t tr = 0, ti = 0, e = 0;
+    // window sample of tap m: x[i - (N-1-m) S]  ->  xs[threadIdx.x + (S-1) + m S]
+    const uint32_t *xw = xs + threadIdx.x + (S - 1);
+    for (unsigned m = 0; m < N; ++m) {
+        const uint32_t w = xw[m * S];
+        const int32_t hr = sext16(w), hi = sext16_hi(w);
+        const int2 c = cs2[m];
+        tr += (uint32_t)hr * (uint32_t)c.x - (uint32_t)hi * (uint32_t)c.y;
+        ti += (uint32_t)hr * (uint32_t)c.y + (uint32_t)hi * (uint32_t)c.x;
+        e += (uint32_t)hr * (uint32_t)hr + (uint32_t)hi * (uint32_t)hi;
+    }
+    const int32_t sr = (int32_t)tr >> (cs & 31u), si = (int32_t)ti >> (cs & 31u);  // scale32 :244
+    const int32_t ar = sr >> 2, ai = si >> 2;                                       // :250
+    corr_out[i] = (uint32_t)ar * (uint32_t)ar + (uint32_t)ai * (uint32_t)ai;
+    en_out[i] = e >> ((unsigned)((int)cs / 2) & 31u);                                // :245
+}
+
+__global__ void corr_detect(const uint32_t *__restrict__ corr, const uint32_t *__restrict__ en, long n,
+                            uint32_t c_prev0, uint32_t c_prev1, uint32_t e_prev0, unsigned *best) {
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const uint32_t c0 = corr[i];
+        const uint32_t c1 = i >= 1 ? corr[i - 1] : c_prev0;
+        const uint32_t c2 = i >= 2 ? corr[i - 2] : (i == 1 ? c_prev0 : c_prev1);
+        const uint32_t e1 = i >= 1 ? en[i - 1] : e_prev0;
+        if (corr_hit(c2, c1, c0, e1)) atomicMin(best, (unsigned)i);
+    }
+}
+
+// new_hist[k] = effective stream sample (last - NSm1 + 1 + k), from input or old history
+__global__ void corr_history(const uint32_t *in, const uint32_t *hist_in, uint32_t *hist_out, long last,
+                             long NSm1) {
+    for (long k = (long)blockIdx.x * blockDim.x + threadIdx.x; k < NSm1; k += (long)gridDim.x * blockDim.x)
+        hist_out[k] = corr_fetch(in, hist_in, last - NSm1 + 1 + k, NSm1);
+}
+
+// ---------------------------------------------------------------- host side
+static int corr_alloc_scratch(srcdsp_corr_state &c, size_t n) {
+    if (n <= c.scratch_cap) return SRCDSP_OK;
+    if (c.d_corr) (void)hipFree(c.d_corr);
+    if (c.d_en) (void)hipFree(c.d_en);
+    c.d_corr = c.d_en = nullptr;
+    SRCDSP_HIP_TRY(hipMalloc(&c.d_corr, 4 * n));
+    SRCDSP_HIP_TRY(hipMalloc(&c.d_en, 4 * n));
+    c.scratch_cap = n;
+    return SRCDSP_OK;
+}
+
+static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *found, int *corr_index,
+                    hipStream_t s) {
+    *found = 0;
+    if (n_ == 0) return SRCDSP_OK;
+    const long n = (long)n_;
+    if (n > 0x7fffffffL) {
+        set_error("corr_step: input longer than INT_MAX samples (correlators.h:212 uses int)");
+        return SRCDSP_ERR_SIZE;
+    }
+    int rc = c.order.before(s);
+    if (rc) return rc;
+    rc = corr_alloc_scratch(c, n_);
+    if (rc) return rc;
+    const long NSm1 = (long)c.NS - 1;
+    const uint32_t *hist = c.d_hist[c.cur];
+    const unsigned cs = (unsigned)c.coeff_scaling;
+    const size_t smem = 4 * (size_t)((kCorrBlock + NSm1 + 3) & ~3l) + 8 * (size_t)c.N;
+    const long blocks = (n + kCorrBlock - 1) / kCorrBlock;
+    hipLaunchKernelGGL(corr_eval, dim3((unsigned)blocks), dim3(kCorrBlock), smem, s, d_in, n, hist, c.d_coef, c.N,
+                       c.S, cs, c.d_corr, c.d_en);
+    SRCDSP_HIP_TRY(hipGetLastError());
+    const unsigned none = 0xffffffffu;
+    SRCDSP_HIP_TRY(hipMemcpyAsync(c.d_best, &none, 4, hipMemcpyHostToDevice, s));
+    const int db = (int)std::max<long>(1, std::min<long>((n + 255) / 256, 4096));
+    hipLaunchKernelGGL(corr_detect, dim3(db), dim3(256), 0, s, c.d_corr, c.d_en, n, c.corr[0], c.corr[1],
+                       c.energy[0], c.d_best);
+    SRCDSP_HIP_TRY(hipGetLastError());
+    unsigned best = none;
+    SRCDSP_HIP_TRY(hipMemcpyAsync(&best, c.d_best, 4, hipMemcpyDeviceToHost, s));
+    SRCDSP_HIP_TRY(hipStreamSynchronize(s));
+
+    const bool hit = best != none;
+    const long last = hit ? (long)best : n - 1;  // last processed sample
+    // registers after processing `last` (correlators.h:228-230, 248-250)
+    uint32_t cw[3] = {0, 0, 0}, ew[3] = {0, 0, 0};
+    const long lo = std::max(0L, last - 2);
+    const long cnt = last - lo + 1;
+    SRCDSP_HIP_TRY(hipMemcpy(cw, c.d_corr + lo, 4 * cnt, hipMemcpyDeviceToHost));
+    SRCDSP_HIP_TRY(hipMemcpy(ew, c.d_en + lo, 4 * cnt, hipMemcpyDeviceToHost));
+    uint32_t nc[3], ne[3];
+    for (int k = 0; k < 3; ++k) {  // nc[k] = corr of sample last-k
+        long idx = last - k;
+        if (idx >= 0) {
+            nc[k] = cw[idx - lo];
+            ne[k] = ew[idx - lo];
+        } else {  // reach back into the previous registers
+            nc[k] = c.corr[-idx - 1];
+            ne[k] = c.energy[-idx - 1];
+        }
+    }
+    if (hit) {
+        // bitSamples (correlators.h:278-288): ring read backwards from the peak
+        // sample best-1 with stride S; with S == 1 the oldest slot already
+        // holds the detected sample (the ring wrapped onto it).
+        std::vector<uint32_t> win((size_t)c.NS + 1);
+        // effective stream positions best-NS .. best
+        const long first = best - (long)c.NS;
+        std::vector<uint32_t> h_hist(NSm1 > 0 ? NSm1 : 1);
+        if (NSm1 > 0) SRCDSP_HIP_TRY(hipMemcpy(h_hist.data(), hist, 4 * NSm1, hipMemcpyDeviceToHost));
+        const long in_lo = std::max(0L, first);
+        const long in_cnt = (long)best - in_lo + 1;
+        std::vector<uint32_t> h_in(in_cnt);
+        SRCDSP_HIP_TRY(hipMemcpy(h_in.data(), d_in + in_lo, 4 * in_cnt, hipMemcpyDeviceToHost));
+        for (long j = first; j <= (long)best; ++j) {
+            uint32_t v;
+            if (j >= 0) v = h_in[j - in_lo];
+            else v = (j + NSm1 >= 0) ? h_hist[j + NSm1] : 0u;
+            win[j - first] = v;
+        }
+        for (unsigned m = 0; m < c.N; ++m) {
+            const long d = (long)(c.N - 1 - m) * c.S;
+            uint32_t v = (d == NSm1) ? win[c.NS] : win[(best - 1 - d) - first];
+            c.bits[2 * m] = (int16_t)(v & 0xffff);
+            c.bits[2 * m + 1] = (int16_t)(v >> 16);
+        }
+    }
+    // history: last NS-1 samples of the effective stream (the detected sample is
+    // overwritten by the next call's first sample)
+    const long last_eff = hit ? (long)best - 1 : n - 1;
+    if (NSm1 > 0) {
+        const int hb = (int)std::max<long>(1, std::min<long>((NSm1 + 255) / 256, 1024));
+        hipLaunchKernelGGL(corr_history, dim3(hb), dim3(256), 0, s, d_in, hist, c.d_hist[c.cur ^ 1], last_eff, NSm1);
+        SRCDSP_HIP_TRY(hipGetLastError());
+        c.cur ^= 1;
+    }
+    for (int k = 0; k < 3; ++k) {
+        c.corr[k] = nc[k];
+        c.energy[k] = ne[k];
+    }
+    if (hit) {
+        *found = 1;
+        *corr_index = (int)best - 1;
+    }
+    return c.order.after(s);
+}
+
+}  // namespace srcdsp
+
+using namespace srcdsp;
+struct srcdsp_corr { srcdsp_corr_state c; };
+
+extern "C" {
+
+SRCDSP_API int srcdsp_corr_create(srcdsp_corr_t *out, unsigned N, unsigned S) {
+    SRCDSP_ARG_CHECK(out != nullptr, "corr_create: null out");
+    *out = nullptr;
+    SRCDSP_ARG_CHECK(N >= 1 && S >= 1 && (unsigned long)N * S <= (1ul << 24), "corr_create: bad N/S");
+    auto *h = new srcdsp_corr();
+    srcdsp_corr_state &c = h->c;
+    c.N = N;
+    c.S = S;
+    c.NS = N * S;
+    c.h_coef.assign(2 * N, 0);
+    c.bits.assign(2 * N, 0);
+    int rc = c.order.init();
+    if (!rc) rc = c.stage.init();
+    if (rc) {
+        delete h;
+        return rc;
+    }
+    const size_t hb = 4 * (size_t)std::max(1u, c.NS - 1);
+    if (hipMalloc(&c.d_coef, 8 * (size_t)N) != hipSuccess || hipMemset(c.d_coef, 0, 8 * (size_t)N) != hipSuccess ||
+        hipMalloc(&c.d_hist[0], hb) != hipSuccess || hipMalloc(&c.d_hist[1], hb) != hipSuccess ||
+        hipMemset(c.d_hist[0], 0, hb) != hipSuccess || hipMalloc(&c.d_best, 4) != hipSuccess) {
+        set_error("corr_create: device allocation failed");
+        srcdsp_corr_destroy(h);
+        return SRCDSP_ERR_HIP;
+    }
+    *out = h;
+    return SRCDSP_OK;
+}
+
+SRCDSP_API int srcdsp_corr_destroy(srcdsp_corr_t h) {
+    if (!h) return SRCDSP_OK;
+    srcdsp_corr_state &c = h->c;
+    (void)c.order.sync();
+    for (void *p : {(void *)c.d_coef, (void *)c.d_hist[0], (void *)c.d_hist[1], (void *)c.d_corr, (void *)c.d_en,
+                    (void *)c.d_best})
+        if (p) (void)hipFree(p);
+    c.order.destroy();
+    c.stage.destroy();
+    delete h;
+    return SRCDSP_OK;
+}
+
+// setPattern (correlators.h:167-194)
+SRCDSP_API int srcdsp_corr_set_pattern(srcdsp_corr_t h, const int32_t *p, double th) {
+    SRCDSP_ARG_CHECK(h != nullptr && p != nullptr, "corr_set_pattern: null argument");
+    srcdsp_corr_state &c = h->c;
+    double tmp = 0;
+    for (unsigned i = 0; i < c.N; ++i) {
+        const int32_t re = p[2 * i], im = (int32_t)(0u - (uint32_t)p[2 * i + 1]);  // conjugate
+        c.h_coef[2 * i] = re;
+        c.h_coef[2 * i + 1] = im;
+        tmp += (double)(int32_t)((uint32_t)re * (uint32_t)re + (uint32_t)im * (uint32_t)im);
+    }
+    if (!(tmp <= 1073217600)) {
+        set_error("setPattern: pattern energy above 1073217600 (correlators.h:185 assert)");
+        return SRCDSP_ERR_ARG;
+    }
+    int rc = c.order.sync();
+    if (rc) return rc;
+    c.coeffs_energy = (uint32_t)(uint64_t)(int64_t)tmp;
+    c.threshold_factor = th * std::sqrt((double)c.coeffs_energy);
+    c.coeff_scaling = cvt_d2i_x86(std::floor(std::log2(std::sqrt((double)c.coeffs_energy))));
+    SRCDSP_HIP_TRY(hipMemcpy(c.d_coef, c.h_coef.data(), 8 * (size_t)c.N, hipMemcpyHostToDevice));
+    return SRCDSP_OK;
+}
+
+// reset (correlators.h:146-159): registers, history and bitSamples cleared
+SRCDSP_API int srcdsp_corr_reset(srcdsp_corr_t h) {
+    SRCDSP_ARG_CHECK(h != nullptr, "corr_reset: null handle");
+    srcdsp_corr_state &c = h->c;
+    int rc = c.order.sync();
+    if (rc) return rc;
+    for (int k = 0; k < 3; ++k) c.energy[k] = c.corr[k] = 0;
+    std::fill(c.bits.begin(), c.bits.end(), 0);
+    const size_t hb = 4 * (size_t)std::max(1u, c.NS - 1);
+    SRCDSP_HIP_TRY(hipMemset(c.d_hist[c.cur], 0, hb));
+    SRCDSP_HIP_TRY(hipDeviceSynchronize());
+    return SRCDSP_OK;
+}
+
+SRCDSP_API int srcdsp_corr_step(srcdsp_corr_t h, const void *d_in, size_t n, int *found, int *corr_index,
+                                void *stream) {
+    SRCDSP_ARG_CHECK(h != nullptr && found != nullptr && corr_index != nullptr, "corr_step: null argument");
+    SRCDSP_ARG_CHECK(d_in != nullptr || n == 0, "corr_step: null input");
+    return corr_run(h->c, (const uint32_t *)d_in, n, found, corr_index, (hipStream_t)stream);
+}
+
+SRCDSP_API int srcdsp_corr_step_host(srcdsp_corr_t h, const void *in, size_t n, int *found, int *corr_index) {
+    SRCDSP_ARG_CHECK(h != nullptr && found != nullptr && corr_index != nullptr, "corr_step_host: null argument");
+    *found = 0;
+    if (n == 0) return SRCDSP_OK;
+    srcdsp_corr_state &c = h->c;
+    int rc = c.stage.reserve(4 * n, 4 * n);
+    if (rc) return rc;
+    memcpy(c.stage.h_buf, in, 4 * n);
+    SRCDSP_HIP_TRY(hipMemcpyAsync(c.stage.d_buf, c.stage.h_buf, 4 * n, hipMemcpyHostToDevice, c.stage.stream));
+    return corr_run(c, (const uint32_t *)c.stage.d_buf, n, found, corr_index, c.stage.stream);
+}
+
+SRCDSP_API int srcdsp_corr_get_bit_samples(srcdsp_corr_t h, int16_t *bits) {
+    SRCDSP_ARG_CHECK(h != nullptr && bits != nullptr, "corr_get_bit_samples: null argument");
+    memcpy(bits, h->c.bits.data(), 4 * (size_t)h->c.N);
+    return SRCDSP_OK;
+}
+
+SRCDSP_API int srcdsp_corr_get_status(srcdsp_corr_t h, uint32_t *e3, uint32_t *c3, uint32_t *ce, int *cs,
+                                      double *tf) {
+    SRCDSP_ARG_CHECK(h != nullptr, "corr_get_status: null handle");
+    const srcdsp_corr_state &c = h->c;
+    for (int k = 0; k < 3; ++k) {
+        if (e3) e3[k] = c.energy[k];
+        if (c3) c3[k] = c.corr[k];
+    }
+    if (ce) *ce = c.coeffs_energy;
+    if (cs) *cs = c.coeff_scaling;
+    if (tf) *tf = c.threshold_factor;
+    return SRCDSP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,256 @@
+"""Parity of the HIP path (through the C ABI) with the reference.
+
+* every golden script (reference outputs, tests/golden) replayed on the GPU,
+  device-resident and host-staged, in both float contracts -- bit-exact;
+* larger seeded cases against the C oracle (pinned to the reference by
+  test_oracle_golden.py) -- bit-exact;
+* the headline size (2^28 samples) through size-independent checks.
+"""
+import numpy as np
+import pytest
+
+from replay import OracleBackend, load_golden, replay
+
+pytestmark = pytest.mark.gpu
+G = load_golden()
+
+
+@pytest.fixture(scope="module")
+def S():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import srcdsp_amd
+    srcdsp_amd.lib()
+    return srcdsp_amd
+
+
+@pytest.fixture(scope="module")
+def O():
+    import pyoracle
+    return {"strict": pyoracle.Oracle(0), "fma": pyoracle.Oracle(1)}
+
+
+def dev(x):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(x)).cuda()
+
+
+# ------------------------------------------------------------------ goldens
+@pytest.mark.parametrize("device", [True, False], ids=["device", "host"])
+@pytest.mark.parametrize("fp", ["fma", "strict"])
+@pytest.mark.parametrize("name", G.names())
+def test_golden_replay_on_gpu(S, name, fp, device):
+    from gpu_backend import GpuBackend
+    fails = replay(G.cases[name], G, GpuBackend(fp, device))
+    assert not fails, "\n".join(fails)
+
+
+# ------------------------------------------------------- decimator, larger
+def _chunks(total, sizes):
+    out, i, k = [], 0, 0
+    while i < total:
+        n = min(sizes[k % len(sizes)], total - i)
+        out.append((i, n))
+        i += n
+        k += 1
+    return out
+
+
+@pytest.mark.parametrize("fp", ["fma", "strict"])
+@pytest.mark.parametrize("ntaps", [127, 128])
+def test_decim_cf32_tile_kernel_vs_oracle(S, O, fp, ntaps):
+    """Headline instantiation through the tile kernel: many tiles, tail tiles,
+    history carried over uneven calls (incl. calls shorter than a tile)."""
+    from srcdsp_amd.design import hamming_sinc
+    c = hamming_sinc(127)
+    if ntaps == 128:
+        c = np.concatenate([c, [0.0]]).astype(np.float32)
+    x = O[fp].gen_cf32(0x5EED, 3, 0, 1 << 20, -32768, 32767)
+    x = x + np.float32(0.37)  # non-integer inputs exercise rounding
+    ref = O[fp].decim(0, 4, c)
+    g = S.FilterDnsamplingFir(c, 4, fp=fp)
+    for off, n in _chunks(len(x), [400000, 8, 2048 * 4 + 4, 131072, 128, 300004]):
+        n -= n % 4
+        if n == 0:
+            continue
+        xs = x[off:off + n]
+        y = g.step(dev(xs)).cpu().numpy()
+        assert np.array_equal(y.view(np.uint32), ref.step(xs).view(np.uint32)), (off, n)
+
+
+def test_decim_fma_vs_strict_tolerance(S, O):
+    """Stated float tolerance: the FMA contract differs from the
+    -O2 x86-64 reference by at most 1 output LSB on at most 1e-4 of outputs."""
+    from srcdsp_amd.design import hamming_sinc
+    c = hamming_sinc(127)
+    x = O["strict"].gen_cf32(0x5EED, 0, 0, 1 << 22)
+    y = S.FilterDnsamplingFir(c, 4, fp="fma").step(dev(x)).cpu().numpy()
+    r = O["strict"].decim(0, 4, c).step(x)
+    d = np.abs(y.view(np.float32) - r.view(np.float32))
+    assert d.max() <= 1.0
+    assert np.count_nonzero(d) <= 1e-4 * d.size
+
+
+def test_decim_ci16_tile_and_mixer_chain_vs_oracle(S, O):
+    from srcdsp_amd.design import hamming_sinc, q14
+    cq = q14(hamming_sinc(127))
+    x = O["strict"].gen_ci16(0x5EED, 1, 0, 1 << 20, -8192, 8191)
+    # plain fixed-point decimator (tile kernel, v_mad_i32_i24)
+    g = S.FilterDnsamplingFir(cq, 4, "complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int32_t")
+    r = O["strict"].decim(1, 4, cq)
+    for off, n in _chunks(len(x), [262144, 4, 1024, 500000]):
+        n -= n % 4
+        xs = x[off:off + n]
+        assert np.array_equal(g.step(dev(xs)).cpu().numpy(), r.step(xs)), (off, n)
+    # config 4: mixer -> decimator fused, against the two reference calls
+    m = S.Mixer(4096)
+    m.reset(0.1)
+    d = S.FilterDnsamplingFir(cq, 4, "complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int32_t")
+    chain = S.MixerDecimatorChain(m, d)
+    om, od = O["strict"].mixer(4096), O["strict"].decim(1, 4, cq)
+    om.reset(0.1)
+    for off, n in _chunks(len(x), [300000, 12, 65536, 700000]):
+        n -= n % 4
+        xs = x[off:off + n]
+        y = chain.step(dev(xs)).cpu().numpy()
+        assert np.array_equal(y, od.step(om.step(xs))), (off, n)
+        assert m.state()[:2] == om.state()[:2]
+
+
+def test_decim_batched_equals_single(S, O):
+    import torch
+    from srcdsp_amd.design import hamming_sinc
+    c = hamming_sinc(127)
+    C, L = 8, 1 << 16
+    x = np.stack([O["fma"].gen_cf32(0x5EED, ch, 0, L) for ch in range(C)])
+    fs = [S.FilterDnsamplingFir(c, 4) for _ in range(C)]
+    xd = dev(x)
+    for rep in range(2):  # two steps: history per channel
+        out = torch.empty((C, L // 4), dtype=torch.complex64, device="cuda")
+        S.decim_step_batched(fs, xd, out)
+        if rep == 0:
+            refs = [O["fma"].decim(0, 4, c) for _ in range(C)]
+        for ch in range(C):
+            assert np.array_equal(out[ch].cpu().numpy(), refs[ch].step(x[ch])), (rep, ch)
+
+
+def test_decim_generic_paths_vs_oracle(S, O):
+    """Unaligned device input and shapes without a tile kernel use the
+    generic kernel; results are still bit-exact."""
+    import torch
+    from srcdsp_amd.design import hamming_sinc
+    x = O["fma"].gen_cf32(7, 0, 0, 40001)
+    c = hamming_sinc(63, 0.06)
+    g = S.FilterDnsamplingFir(c, 8)
+    r = O["fma"].decim(0, 8, c)
+    assert np.array_equal(g.step(dev(x[:40000])).cpu().numpy(), r.step(x[:40000]))
+    # misaligned (8-byte offset) input through the M=4 path
+    c127 = hamming_sinc(127)
+    g4, r4 = S.FilterDnsamplingFir(c127, 4), O["fma"].decim(0, 4, c127)
+    buf = dev(x)  # 40001 samples; view starting at sample 1 is 8-B aligned only
+    view = buf[1:40001]
+    assert np.array_equal(g4.step(view).cpu().numpy(), r4.step(x[1:40001]))
+    del torch
+
+
+def test_decim_errors_and_empty(S):
+    import torch
+    from srcdsp_amd._capi import ERR_SIZE, SrcdspError
+    g = S.FilterDnsamplingFir(np.ones(5, np.float32), 4)
+    with pytest.raises(SrcdspError) as e:
+        g.step(torch.zeros(10, dtype=torch.complex64, device="cuda"), torch.zeros(2, dtype=torch.complex64,
+                                                                                 device="cuda"))
+    assert e.value.code == ERR_SIZE
+    out = g.step(torch.zeros(0, dtype=torch.complex64, device="cuda"))
+    assert out.numel() == 0
+    with pytest.raises(TypeError):
+        S.FilterDnsamplingFir(np.ones(5, np.float32), 4, "float", "float", "float", "float")
+    d2 = S.FilterDnsamplingFir(np.ones(8, np.float32), 4)
+    with pytest.raises(SrcdspError):
+        d2.setCoeffs(np.ones(7, np.float32))  # dsptl_dnsampling_filters.h:122 assert
+
+
+def test_headline_size_properties(S, O):
+    """Config 2 at full size (2^28 samples, device-resident): spot-check output
+    windows against the oracle run on the same input windows (first tiles,
+    tile seams, random interior, last tile) -- size-independent parity."""
+    import torch
+    from srcdsp_amd.design import hamming_sinc
+    c = hamming_sinc(127)
+    L = 1 << 28
+    x = torch.empty(L, dtype=torch.complex64, device="cuda")
+    S.fill_synthetic(x, "cf32", seed=0x5EED, channel=0)
+    y = S.FilterDnsamplingFir(c, 4, fp="fma").step(x)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(1)
+    n_out = L // 4
+    starts = [0, 2048 - 3, 4096 - 3, n_out - 1000] + list(rng.integers(40, n_out - 1000, 12))
+    for s0 in starts:
+        s0 = int(s0)
+        lo = max(0, 4 * s0 - 128)
+        xin = x[lo:4 * (s0 + 64)].cpu().numpy()
+        host = O["fma"].gen_cf32(0x5EED, 0, lo, len(xin))
+        assert np.array_equal(xin, host)  # device generator == host generator
+        ref = O["fma"].decim(0, 4, c)
+        pre = (4 * s0 - lo) // 4
+        r = ref.step(xin)[pre:]
+        got = y[s0:s0 + 64].cpu().numpy()
+        assert np.array_equal(got, r[:len(got)]), s0
+    del x, y
+    torch.cuda.empty_cache()
+
+
+# ----------------------------------------------------- other operators
+def test_mixer_large_vs_oracle(S, O):
+    x = O["fma"].gen_ci16(11, 0, 0, (1 << 20) + 3, -32768, 32767)
+    for N, f in ((4096, 0.1), (1024, -0.37), (256, 0.999)):
+        m, r = S.Mixer(N), O["fma"].mixer(N)
+        m.reset(f)
+        r.reset(f)
+        for off, n in _chunks(len(x), [333333, 1, 65536, 400000]):
+            xs = x[off:off + n]
+            assert np.array_equal(m.step(dev(xs)).cpu().numpy(), r.step(xs)), (N, off)
+            assert m.state()[:2] == r.state()[:2]
+
+
+def test_upsampler_vs_oracle(S, O):
+    from srcdsp_amd.design import hamming_sinc, q14
+    c = q14(hamming_sinc(32, 0.12) * 4)
+    x = O["fma"].gen_ci16(5, 0, 0, 1 << 16, -8192, 8191)
+    for it in (False, True):
+        g = S.FilterUpsamplingFir(c if not it else c // 8, 4)
+        r = O["fma"].up(0, 4, c if not it else c // 8)
+        for off, n in _chunks(len(x), [30000, 3, 20000]):
+            xs = x[off:off + n]
+            last = off + n >= len(x)
+            assert np.array_equal(g.step(dev(xs), None, last, it).cpu().numpy(), r.step(xs, last, it)), (it, off)
+
+
+@pytest.mark.parametrize("N,S_", [(1024, 1), (32, 4), (64, 2)])
+def test_correlator_vs_oracle(S, O, N, S_):
+    from srcdsp_amd.design import qpsk_pattern
+    p = qpsk_pattern(N, 500, seed=N)
+    rng = np.random.default_rng(N)
+    n = 1 << 16 if N == 1024 else 1 << 17
+    x = rng.integers(-125, 126, size=(n, 2)).astype(np.int32)
+    for off in (n // 3, (3 * n) // 4):
+        for m in range(N):
+            if off + m * S_ < n:
+                x[off + m * S_] += 2 * p[m]
+    x = np.clip(x, -32768, 32767).astype(np.int16)
+    g, r = S.FixedPatternCorrelator(N, S_), O["fma"].corr(N, S_)
+    g.setPattern(p)
+    r.set_pattern(p)
+    pos, events = 0, 0
+    while pos < n:  # keep stepping after detections, like a receiver would
+        xs = x[pos:pos + 20000]
+        fg, ig = g.step(dev(xs))
+        fr, ir = r.step(xs)
+        assert (fg, fg and ig) == (fr, fr and ir)
+        assert np.array_equal(g.getRefBitSamples(), r.bit_samples())
+        st, sr = g.getStatus(), r.status()
+        assert all(st[k] == sr[k] for k in ("energy", "corr", "coeffs_energy", "coeff_scaling"))
+        events += fr
+        pos += (ir + 2) if fr else len(xs)
+    assert events >= 1
