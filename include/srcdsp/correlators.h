@@ -1,0 +1,96 @@
+/*
+ * Drop-in for SrcDsp's correlators.h:
+ * dsptl::FixedPatternCorrelator<int16_t, int32_t, N, S>
+ * (reference correlators.h:54-316), executed by libsrcdsp_hip.so.
+ */
+#ifndef SRCDSP_DROPIN_CORRELATORS_H
+#define SRCDSP_DROPIN_CORRELATORS_H
+
+#include <array>
+#include <sstream>
+
+#include "srcdsp_dropin_common.h"
+
+namespace dsptl {
+
+template <class InType = int16_t, class CompType = int32_t, size_t N = 32, size_t S = 4>
+class FixedPatternCorrelator {
+    static_assert(std::is_same<InType, int16_t>::value && std::is_same<CompType, int32_t>::value,
+                  "FixedPatternCorrelator is provided for <int16_t, int32_t, N, S>");
+
+public:
+    /// correlators.h:59-81 (InputEnergy is never written by the reference; 0 here)
+    struct CorrState {
+        static const int Nelements = 3;
+        float InputEnergy;
+        uint32_t coeffsEnergy;
+        int coeffScaling;
+        uint32_t energyValue[Nelements];
+        uint32_t corrValue[Nelements];
+        double thresholdFactor;
+        std::string prettyString() {
+            std::ostringstream os;
+            os << "Input Energy: " << InputEnergy << '\n';
+            os << "Coeffs Energy: " << coeffsEnergy << '\n';
+            os << "Coeff Scaling: " << coeffScaling << '\n';
+            os << "Threshold Factor: " << thresholdFactor << '\n';
+            for (int i = 0; i < Nelements; ++i) os << "Energy Value " << i << ": " << energyValue[i] << '\n';
+            for (int i = 0; i < Nelements; ++i) os << "CorrValue " << i << ": " << corrValue[i] << '\n';
+            return os.str();
+        }
+    };
+
+    /// correlators.h:119-132
+    FixedPatternCorrelator() : h_(nullptr) {
+        srcdsp_detail::check(srcdsp_corr_create(&h_, (unsigned)N, (unsigned)S), "FixedPatternCorrelator");
+    }
+    ~FixedPatternCorrelator() { srcdsp_corr_destroy(h_); }
+    FixedPatternCorrelator(const FixedPatternCorrelator &) = delete;
+    FixedPatternCorrelator &operator=(const FixedPatternCorrelator &) = delete;
+
+    /// correlators.h:209-303
+    bool step(const std::vector<std::complex<InType>> &in, int &corrIndex) {
+        int found = 0, idx = corrIndex;
+        srcdsp_detail::check(srcdsp_corr_step_host(h_, in.data(), in.size(), &found, &idx), "step");
+        if (found) corrIndex = idx;
+        return found != 0;
+    }
+    bool step(const DeviceSpan<const std::complex<InType>> &in, int &corrIndex, void *stream = nullptr) {
+        int found = 0, idx = corrIndex;
+        srcdsp_detail::check(srcdsp_corr_step(h_, in.data, in.size, &found, &idx, stream), "step(device)");
+        if (found) corrIndex = idx;
+        return found != 0;
+    }
+    /// correlators.h:167-194
+    void setPattern(const std::array<std::complex<CompType>, N> &in, double thresholdCoeff = 0.8) {
+        std::vector<int32_t> p(2 * N);
+        for (size_t i = 0; i < N; ++i) {
+            p[2 * i] = in[i].real();
+            p[2 * i + 1] = in[i].imag();
+        }
+        srcdsp_detail::check(srcdsp_corr_set_pattern(h_, p.data(), thresholdCoeff), "setPattern");
+    }
+    /// correlators.h:146-159
+    void reset() { srcdsp_detail::check(srcdsp_corr_reset(h_), "reset"); }
+    /// correlators.h:311-316
+    std::vector<std::complex<InType>> getRefBitSamples() {
+        std::vector<std::complex<InType>> b(N);
+        srcdsp_detail::check(srcdsp_corr_get_bit_samples(h_, reinterpret_cast<int16_t *>(b.data())),
+                             "getRefBitSamples");
+        return b;
+    }
+    /// correlators.h:90
+    CorrState getStatus() {
+        CorrState s{};
+        srcdsp_detail::check(srcdsp_corr_get_status(h_, s.energyValue, s.corrValue, &s.coeffsEnergy,
+                                                    &s.coeffScaling, &s.thresholdFactor),
+                             "getStatus");
+        return s;
+    }
+
+private:
+    srcdsp_corr_t h_;
+};
+
+}  // namespace dsptl
+#endif

@@ -1,0 +1,64 @@
+/*
+ * srcdsp_dropin_common.h -- shared pieces of the C++ drop-in headers
+ * (the headers in include/srcdsp), which keep SrcDsp's class templates, namespaces and
+ * step() signatures and forward every call to libsrcdsp_hip.so's C ABI.
+ *
+ * Build a reference user's code against them by replacing the include path of
+ * the SrcDsp tree with include/srcdsp and linking libsrcdsp_hip.so.
+ *
+ * Errors: where the reference asserts, these wrappers assert too; with NDEBUG
+ * (where the reference has undefined behaviour) they throw std::runtime_error.
+ */
+#ifndef SRCDSP_DROPIN_COMMON_H
+#define SRCDSP_DROPIN_COMMON_H
+
+#include <cassert>
+#include <complex>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "../srcdsp_hip.h"
+
+namespace dsptl {
+
+/// A device-resident buffer (HIP device pointer + element count) for the
+/// device overloads of step(); the host std::vector overloads stage through
+/// pinned memory and are PCIe-bound.
+template <class T>
+struct DeviceSpan {
+    T *data;
+    size_t size;
+};
+
+namespace srcdsp_detail {
+
+inline void check(int rc, const char *what) {
+    if (rc != SRCDSP_OK) {
+        std::string msg = std::string(what) + ": " + srcdsp_last_error();
+        assert(!"libsrcdsp_hip call failed" && what);
+        throw std::runtime_error(msg);
+    }
+}
+
+template <class T> struct kind;  // sample / coefficient type codes
+template <> struct kind<std::complex<float>> { static constexpr int v = 0; };
+template <> struct kind<std::complex<int16_t>> { static constexpr int v = 1; };
+template <> struct kind<std::complex<int32_t>> { static constexpr int v = 2; };
+template <> struct kind<float> { static constexpr int v = 3; };
+template <> struct kind<int16_t> { static constexpr int v = 4; };
+template <> struct kind<int32_t> { static constexpr int v = 5; };
+
+constexpr int code4(int a, int b, int c, int d) { return ((a * 8 + b) * 8 + c) * 8 + d; }
+
+template <class In, class Out, class Internal, class Coef>
+constexpr int code_of() {
+    return code4(kind<In>::v, kind<Out>::v, kind<Internal>::v, kind<Coef>::v);
+}
+
+}  // namespace srcdsp_detail
+}  // namespace dsptl
+
+#endif

@@ -212,7 +212,7 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
         // holds the detected sample (the ring wrapped onto it).
         std::vector<uint32_t> win((size_t)c.NS + 1);
         // effective stream positions best-NS .. best
-        const long first = best - (long)c.NS;
+        const long first = (long)best - (long)c.NS;
         std::vector<uint32_t> h_hist(NSm1 > 0 ? NSm1 : 1);
         if (NSm1 > 0) SRCDSP_HIP_TRY(hipMemcpy(h_hist.data(), hist, 4 * NSm1, hipMemcpyDeviceToHost));
         const long in_lo = std::max(0L, first);
@@ -227,7 +227,7 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
         }
         for (unsigned m = 0; m < c.N; ++m) {
             const long d = (long)(c.N - 1 - m) * c.S;
-            uint32_t v = (d == NSm1) ? win[c.NS] : win[(best - 1 - d) - first];
+            uint32_t v = (d == NSm1) ? win[c.NS] : win[((long)best - 1 - d) - first];
             c.bits[2 * m] = (int16_t)(v & 0xffff);
             c.bits[2 * m + 1] = (int16_t)(v >> 16);
         }

@@ -1,0 +1,142 @@
+"""The C++ drop-in headers (include/srcdsp/): reference-style code builds
+against them unchanged and reproduces the reference's results.
+
+CPU: every supported instantiation compiles; an instantiation the reference
+cannot compile fails to compile here too.  GPU: tests/cpp/dropin_main.cpp runs
+on the box and its outputs are compared bit-exactly with the oracle."""
+import os
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+INC = os.path.join(ROOT, "include", "srcdsp")
+LIBDIR = os.path.join(ROOT, "srcdsp_amd", "lib")
+
+
+def _compile(src_text, out, tmp, link=False):
+    src = os.path.join(tmp, "t.cpp")
+    with open(src, "w") as f:
+        f.write(src_text)
+    cmd = ["g++", "-std=c++14", "-Wall", "-I", INC, src, "-o", out]
+    if link:
+        cmd += ["-L", LIBDIR, "-lsrcdsp_hip", f"-Wl,-rpath,{LIBDIR}", "-Wl,-rpath,/opt/rocm/lib"]
+    else:
+        cmd = cmd[:-2] + ["-fsyntax-only"]
+    return subprocess.run(cmd, capture_output=True, text=True)
+
+
+def test_dropin_headers_compile_all_supported_instantiations(tmp_path):
+    src = """
+#include "dnsampling_filters.h"
+#include "filters.h"
+#include "upsampling_filters.h"
+#include "mixers.h"
+#include "correlators.h"
+using cf32 = std::complex<float>; using ci16 = std::complex<int16_t>; using ci32 = std::complex<int32_t>;
+template class dsptl::FilterDnsamplingFir<cf32, cf32, cf32, float, 4>;
+template class dsptl::FilterDnsamplingFir<ci16, ci16, ci32, int32_t, 4>;
+template class dsptl::FilterDnsamplingFir<ci16, ci16, ci32, int16_t, 2>;
+template class dsptl::FilterDnsamplingFir<ci32, ci16, ci32, int32_t, 8>;
+template class FilterFir<cf32, cf32, cf32, float>;
+template class FilterFir<float, cf32, float, float>;
+template class FilterFir<ci16, ci16, ci32, int32_t>;
+template class dsptl::FilterUpsamplingFir<ci16, ci16, ci32, int32_t, 4>;
+template class dsptl::FilterUpsamplingFir<ci16, ci16, ci32, int16_t, 4>;
+template class dsptl::FilterUpsamplingFir<int16_t, int16_t, int32_t, int32_t, 2>;
+template class dsptl::Mixer<ci16, ci16, int16_t, 4096>;
+template class dsptl::FixedPatternCorrelator<int16_t, int32_t, 1024, 1>;
+template class dsptl::FixedPatternCorrelator<int16_t, int32_t, 32, 4>;
+int main() { return 0; }
+"""
+    r = _compile(src, str(tmp_path / "a.out"), str(tmp_path))
+    assert r.returncode == 0, r.stderr
+
+
+@pytest.mark.parametrize("inst", [
+    "dsptl::FilterDnsamplingFir<float, float, float, float, 4>",        # dsptl_dnsampling_filters.h:215
+    "FilterFir<float, float, float, float>",                            # filters.h:164
+    "dsptl::FilterUpsamplingFir<std::complex<float>, std::complex<float>, std::complex<float>, float, 4>",
+])
+def test_dropin_rejects_what_the_reference_cannot_compile(tmp_path, inst):
+    src = ('#include "dnsampling_filters.h"\n#include "filters.h"\n#include "upsampling_filters.h"\n'
+           f"template class {inst};\nint main(){{return 0;}}\n")
+    r = _compile(src, str(tmp_path / "a.out"), str(tmp_path))
+    assert r.returncode != 0
+
+
+def _rec(f, tag, arr):
+    b = np.ascontiguousarray(arr).tobytes()
+    f.write(struct.pack("<iq", tag, len(b)))
+    f.write(b)
+
+
+def _read(path):
+    out = {}
+    with open(path, "rb") as f:
+        while True:
+            h = f.read(12)
+            if len(h) < 12:
+                return out
+            tag, nb = struct.unpack("<iq", h)
+            out[tag] = f.read(nb)
+
+
+@pytest.mark.gpu
+def test_dropin_program_matches_oracle(tmp_path):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import pyoracle
+    from srcdsp_amd.design import hamming_sinc, q14, qpsk_pattern
+    exe = str(tmp_path / "dropin_main")
+    r = subprocess.run(["g++", "-std=c++14", "-O2", "-I", INC, os.path.join(ROOT, "tests", "cpp", "dropin_main.cpp"),
+                        "-o", exe, "-L", LIBDIR, "-lsrcdsp_hip", f"-Wl,-rpath,{LIBDIR}", "-Wl,-rpath,/opt/rocm/lib"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    O = pyoracle.Oracle(1)
+    c = hamming_sinc(127)
+    cq = q14(c)
+    x = O.gen_cf32(1, 0, 0, 40000)
+    xi = O.gen_ci16(2, 0, 0, 20000, -8192, 8191)
+    cf = hamming_sinc(31, 0.2)
+    xf = np.random.default_rng(3).integers(-2048, 2048, 5000).astype(np.float32)
+    cu = q14(hamming_sinc(32, 0.12) * 4)
+    p = qpsk_pattern(32, 500, seed=1)
+    xc = np.random.default_rng(4).integers(-125, 126, size=(6000, 2)).astype(np.int32)
+    for m in range(32):
+        xc[3000 + 4 * m] += 2 * p[m]
+    xc = xc.astype(np.int16)
+    fin = tmp_path / "in.bin"
+    with open(fin, "wb") as f:
+        for tag, a in ((1, c), (2, x), (3, xi), (4, cq), (5, cf), (6, xf), (7, cu), (8, p), (9, xc)):
+            _rec(f, tag, a)
+    r = subprocess.run([exe, str(fin), str(tmp_path / "out.bin")], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = _read(tmp_path / "out.bin")
+
+    d = O.decim(0, 4, c)
+    h = (len(x) // 2) & ~3
+    exp = np.concatenate([d.step(x[:h]), d.step(x[h:])])
+    assert got[101] == exp.tobytes()
+    assert got[102] == O.decim(1, 4, cq).step(xi).tobytes()
+    mix = O.mixer(4096)
+    mix.reset(0.1)
+    mixed = mix.step(xi)
+    assert got[103] == mixed.tobytes()
+    assert got[104] == O.decim(1, 4, cq).step(mixed).tobytes()
+    assert got[105] == O.fir(1, cf).step(xf).tobytes()
+    u = O.up(0, 4, cu)
+    exp_u = np.concatenate([u.step(xi[:1000]), u.step(xi[1000:1500], flush=True, iterator=True)])
+    assert got[106] == exp_u.tobytes()
+    corr = O.corr(32, 4)
+    corr.set_pattern(p)
+    found, idx = corr.step(xc)
+    st = corr.status()
+    res = np.frombuffer(got[107], np.int32)
+    assert res[0] == int(found) and (not found or res[1] == idx)
+    assert list(res[2:]) == [np.int32(np.uint32(st["corr"][0])), np.int32(np.uint32(st["energy"][0])),
+                             st["coeff_scaling"]]
+    assert got[108] == corr.bit_samples().tobytes()
