@@ -74,16 +74,6 @@ def barrier(world):
     torch.cuda.synchronize()
 
 
-def max_over_ranks(x, world):
-    import torch
-    if world == 1:
-        return x
-    import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
-
-
 # ---------------------------------------------------------------- workloads
 class Workload:
     """One step = one pass of the hot path over one batch of resident input."""
@@ -247,6 +237,7 @@ def main():
     import torch
     world, rank, local = dist_setup(args)
     import srcdsp_amd as S
+    from srcdsp_amd.dist import gather_to_root, max_over_ranks
     S.lib()  # loud failure if the HIP library is missing
     L = args.samples - args.samples % 4
     work = WORKLOADS[args.workload](S, torch, L, args.channels_per_gpu, rank, args.fp)
@@ -266,7 +257,7 @@ def main():
         ev[i][1].record(stream)
     barrier(world)
     t1 = time.perf_counter()
-    wall = max_over_ranks(t1 - t0, world)
+    wall = max_over_ranks(t1 - t0, world, device="cuda")
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     kern_avg_ms = float(np.mean(kern_ms))
 
@@ -278,12 +269,9 @@ def main():
     gather_ms = None
     if world > 1 and not args.no_gather and args.workload == "decim":
         # configs[2]: gather every rank's decimated channels to rank 0 over RCCL (xGMI)
-        import torch.distributed as dist
-        y = work.y
-        bufs = [torch.empty_like(y) for _ in range(world)] if rank == 0 else None
         barrier(world)
         g0 = time.perf_counter()
-        dist.gather(y, bufs, dst=0)
+        bufs = gather_to_root(work.y, world, rank)
         barrier(world)
         gather_ms = (time.perf_counter() - g0) * 1e3
         del bufs

@@ -1,0 +1,71 @@
+// Tuning harness (not part of the product): instantiates decimator kernel
+// variants from srcdsp_amd/csrc/decim_kernels.h and an FMA-rate microbenchmark
+// so they can be timed side by side, interleaved, in one process.
+#include "../../srcdsp_amd/csrc/decim_kernels.h"
+
+using namespace srcdsp;
+
+// ---- FMA issue-rate microbenchmark: 16 independent chains per lane
+template <int MODE>
+__global__ __launch_bounds__(256) void fma_rate(float *out, int iters, float c0) {
+    float a[16];
+    float2 p[8];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) a[j] = threadIdx.x * 0.001f + j;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) p[j] = make_float2(a[2 * j], a[2 * j + 1]);
+    const float2 cc = make_float2(c0, c0);
+    const float2 xx = make_float2(1.0001f, 0.9999f);
+    for (int i = 0; i < iters; ++i) {
+        if constexpr (MODE == 0) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(a[j]) : "s"(c0), "v"(xx.x));
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(p[j]) : "v"(cc), "v"(xx));
+        }
+    }
+    float s = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) s += a[j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += p[j].x + p[j].y;
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+extern "C" int tune_fma_rate(int mode, int blocks, int iters, float *out, void *stream) {
+    if (mode == 0)
+        hipLaunchKernelGGL(fma_rate<0>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, out, iters, 1.0f);
+    else
+        hipLaunchKernelGGL(fma_rate<1>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, out, iters, 1.0f);
+    return hipGetLastError();
+}
+
+// ---- decimator variants (cf32, M=4, 127 taps, FMA)
+template <class K>
+static int launch(K kern, int blocks, int threads, const DecimLaunch &L, hipStream_t s) {
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), 0, s, L);
+    return hipGetLastError();
+}
+
+extern "C" int tune_decim(int variant, int grid, const float *d_coef, const void *in, void *out, long n_in,
+                          const void *hist_in, void *hist_out, void *stream) {
+    DecimLaunch L{};
+    L.in = in; L.out = out; L.n_in = n_in; L.n_out = n_in / 4; L.ntaps = 127; L.shift = 0;
+    L.hist_in[0] = hist_in; L.hist_out[0] = hist_out;
+    L.coef = d_coef;
+    hipStream_t s = (hipStream_t)stream;
+    auto tiles = [&](int TO) { return (L.n_out + TO - 1) / TO; };
+    switch (variant) {
+    case 0: L.ntiles = tiles(256 * 8); return launch(decim_tile_cf32<127, 8, 256, true>, (int)L.ntiles, 256, L, s);
+    case 1: L.ntiles = tiles(256 * 4); return launch(decim_tile_cf32<127, 4, 256, true>, (int)L.ntiles, 256, L, s);
+    case 2: L.ntiles = tiles(128 * 8); return launch(decim_tile_cf32<127, 8, 128, true>, (int)L.ntiles, 128, L, s);
+    case 3: L.ntiles = tiles(256 * 8); return launch(decim_stream_cf32<127, 8, 256, true>, grid, 256, L, s);
+    case 4: L.ntiles = tiles(256 * 4); return launch(decim_stream_cf32<127, 4, 256, true>, grid, 256, L, s);
+    case 5: L.ntiles = tiles(128 * 8); return launch(decim_stream_cf32<127, 8, 128, true>, grid, 128, L, s);
+    case 6: L.ntiles = tiles(64 * 8); return launch(decim_stream_cf32<127, 8, 64, true>, grid, 64, L, s);
+    case 7: L.ntiles = tiles(256 * 6); return launch(decim_stream_cf32<127, 6, 256, true>, grid, 256, L, s);
+    default: return -1;
+    }
+}

@@ -29,398 +29,39 @@
 
 #include "ops.h"
 
+#include "decim_kernels.h"
+
 namespace srcdsp {
-
-// Taps of the tile kernels travel in the kernel-argument segment: wave-uniform
-// constant memory, fetched with s_load into SGPRs and consumed as the scalar
-// operand of each FMA (a pointer to global taps could alias the outputs, which
-// forces vector loads into VGPRs).
-constexpr int kMaxTileTaps = 128;
-struct TapsF { float c[kMaxTileTaps]; };
-struct TapsI { int32_t c[kMaxTileTaps]; };
-
-// ------------------------------------------------------------ arithmetic
-template <bool FMA>
-__device__ __forceinline__ float mac(float c, float x, float y) {
-    if constexpr (FMA) return __builtin_fmaf(c, x, y);
-    else return y + x * c;  // -ffp-contract=off: rounded product, then rounded sum
-}
-
-__device__ __forceinline__ float q16f(float y, unsigned shift) {
-    return (float)limit16(cvt_f2i_x86(y), shift);
-}
-
-// read one input sample of channel data / history; idx may be negative (history)
-template <typename T>
-__device__ __forceinline__ T fetch(const T *in, const T *hist, long idx, long n_in, int H) {
-    if (idx >= 0) return idx < n_in ? in[idx] : T{};
-    long h = idx + H;
-    return h >= 0 ? hist[h] : T{};
-}
-
-// ---------------------------------------------------------------- history
-// hist_out[k] = (hist_in ++ in)[H + n_in - H + k], k < H
-template <typename T>
-__device__ void write_history(const T *in, long n_in, const T *hist_in, T *hist_out, int H) {
-    for (int k = threadIdx.x; k < H; k += blockDim.x) {
-        long idx = n_in - H + k;
-        hist_out[k] = idx >= 0 ? in[idx] : hist_in[H + idx];
-    }
-}
-
-// ================================================================ generic
-template <int KV, bool FMA>
-__global__ void decim_generic(DecimLaunch a, unsigned M) {
-    const int ch = blockIdx.y;
-    const int N = a.ntaps, H = N - 1;
-    const long n_out = a.n_out, n_in = a.n_in;
-    if (blockIdx.x == 0) {
-        if constexpr (KV == KV_CF32 || KV == KV_CI32_I32) {
-            write_history((const uint2 *)a.in + ch * a.in_stride, n_in, (const uint2 *)a.hist_in[ch],
-                          (uint2 *)a.hist_out[ch], H);
-        } else {
-            write_history((const uint32_t *)a.in + ch * a.in_stride, n_in, (const uint32_t *)a.hist_in[ch],
-                          (uint32_t *)a.hist_out[ch], H);
-        }
-    }
-    for (long o = (long)blockIdx.x * blockDim.x + threadIdx.x; o < n_out; o += (long)gridDim.x * blockDim.x) {
-        const long j = o * (long)M;
-        if constexpr (KV == KV_CF32) {
-            const float2 *in = (const float2 *)a.in + ch * a.in_stride;
-            const float2 *hist = (const float2 *)a.hist_in[ch];
-            const float *c = (const float *)a.coef;
-            float yr = 0.f, yi = 0.f;
-            for (int k = 0; k < N; ++k) {
-                float2 x = fetch(in, hist, j - k, n_in, H);
-                yr = mac<FMA>(c[k], x.x, yr);
-                yi = mac<FMA>(c[k], x.y, yi);
-            }
-            ((float2 *)a.out + ch * a.out_stride)[o] = make_float2(q16f(yr, a.shift), q16f(yi, a.shift));
-        } else if constexpr (KV == KV_F32_REAL) {
-            const float *in = (const float *)a.in + ch * a.in_stride;
-            const float *hist = (const float *)a.hist_in[ch];
-            const float *c = (const float *)a.coef;
-            float y = 0.f;
-            for (int k = 0; k < N; ++k) y = mac<FMA>(c[k], fetch(in, hist, j - k, n_in, H), y);
-            ((float2 *)a.out + ch * a.out_stride)[o] = make_float2(q16f(y, a.shift), 0.f);
-        } else if constexpr (KV == KV_CI32_I32) {
-            const int2 *in = (const int2 *)a.in + ch * a.in_stride;
-            const int2 *hist = (const int2 *)a.hist_in[ch];
-            const int32_t *c = (const int32_t *)a.coef;
-            uint32_t yr = 0, yi = 0;
-            for (int k = 0; k < N; ++k) {
-                int2 x = fetch(in, hist, j - k, n_in, H);
-                yr += (uint32_t)c[k] * (uint32_t)x.x;
-                yi += (uint32_t)c[k] * (uint32_t)x.y;
-            }
-            ((uint32_t *)a.out + ch * a.out_stride)[o] =
-                pack16(limit16((int32_t)yr, a.shift), limit16((int32_t)yi, a.shift));
-        } else {  // KV_CI16_I32, KV_CI16_I16
-            const uint32_t *in = (const uint32_t *)a.in + ch * a.in_stride;
-            const uint32_t *hist = (const uint32_t *)a.hist_in[ch];
-            const int32_t *c = (const int32_t *)a.coef;
-            uint32_t yr = 0, yi = 0;
-            for (int k = 0; k < N; ++k) {
-                uint32_t w = fetch(in, hist, j - k, n_in, H);
-                uint32_t pr = (uint32_t)c[k] * (uint32_t)sext16(w);
-                uint32_t pi = (uint32_t)c[k] * (uint32_t)sext16_hi(w);
-                if constexpr (KV == KV_CI16_I16) {  // std::operator*(short, complex<short>): int16 wrap
-                    pr = (uint32_t)sext16(pr);
-                    pi = (uint32_t)sext16(pi);
-                }
-                yr += pr;
-                yi += pi;
-            }
-            ((uint32_t *)a.out + ch * a.out_stride)[o] =
-                pack16(limit16((int32_t)yr, a.shift), limit16((int32_t)yi, a.shift));
-        }
-    }
-}
-
-// ============================================================ cf32 tiles
-// Tile geometry for complex<float>, M = 4: a granule is 16 B = 2 samples,
-// a 4-sample polyphase group is 2 granules.  LDS granule of tile granule g:
-//   L(g) = g + (g - 2NQ + KPAD*PR) / PR, PR = 2R granules per lane chunk,
-// i.e. one pad granule in front of every lane chunk, so lane t's chunk starts
-// at B_t = 2NQ + KPAD + (2R+1) t and 16 lanes of a ds_read_b128 group hit 16
-// distinct 16-B bank slots.
-template <int NT, int R, int BLOCK, bool FMA>
-__global__ __launch_bounds__(BLOCK) void decim_tile_cf32(DecimLaunch a, TapsF taps) {
-    constexpr int NQ = (NT + 3) / 4;
-    constexpr int TO = BLOCK * R;
-    constexpr int TG = 2 * TO + 2 * NQ;
-    constexpr int PR = 2 * R;
-    constexpr int KPAD = ceildiv(2 * NQ, PR);
-    constexpr int LG = TG + (TG + KPAD * PR) / PR + 1;
-    constexpr int PER = ceildiv(TG, BLOCK);
-    __shared__ float4 lds[LG];
-
-    const int ch = blockIdx.y;
-    const float2 *in = (const float2 *)a.in + ch * a.in_stride;
-    const float2 *hist = (const float2 *)a.hist_in[ch];
-    const long n_in = a.n_in;
-    const int H = NT - 1;
-    const long tile = xcd_tile(blockIdx.x, gridDim.x);
-    const long o0 = tile * TO;
-    const long b0 = 4 * o0 - 4 * NQ;
-    const int t = threadIdx.x;
-
-    if (tile == 0) write_history(in, n_in, hist, (float2 *)a.hist_out[ch], H);
-
-    // ---- stage the tile: HBM -> VGPR -> LDS (all loads issued before any write)
-    float4 v[PER];
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int g = t + i * BLOCK;
-        const long s = b0 + 2 * (long)g;
-        if (g < TG) {
-            if (s >= 0 && s + 1 < n_in) {
-                v[i] = *(const float4 *)(in + s);
-            } else {
-                float2 lo = fetch(in, hist, s, n_in, H), hi = fetch(in, hist, s + 1, n_in, H);
-                v[i] = make_float4(lo.x, lo.y, hi.x, hi.y);
-            }
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int g = t + i * BLOCK;
-        if (g < TG) lds[g + (g - 2 * NQ + KPAD * PR) / PR] = v[i];
-    }
-    __syncthreads();
-
-    // ---- compute: lane t owns outputs n0 .. n0+R-1
-    const int Bt = 2 * NQ + KPAD + (PR + 1) * t;
-    float2 X[4 * (NQ + R)];  // X[s + 4NQ] = x[4 n0 + s]
-    float yr[R], yi[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) yr[r] = yi[r] = 0.f;
-
-    auto load_group = [&](int e) {  // samples 4e .. 4e+3 relative to 4 n0
-        const float4 g0 = lds[Bt + 2 * e + floordiv(2 * e, PR)];
-        const float4 g1 = lds[Bt + 2 * e + 1 + floordiv(2 * e + 1, PR)];
-        X[4 * e + 4 * NQ + 0] = make_float2(g0.x, g0.y);
-        X[4 * e + 4 * NQ + 1] = make_float2(g0.z, g0.w);
-        X[4 * e + 4 * NQ + 2] = make_float2(g1.x, g1.y);
-        X[4 * e + 4 * NQ + 3] = make_float2(g1.z, g1.w);
-    };
-#pragma unroll
-    for (int e = -1; e < R; ++e) load_group(e);
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        if (q + 1 < NQ) load_group(-q - 2);
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            const int k = 4 * q + p;
-            if (k < NT) {
-                const float c = taps.c[k];
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const float2 x = X[4 * (r - q) - p + 4 * NQ];
-                    yr[r] = mac<FMA>(c, x.x, yr[r]);
-                    yi[r] = mac<FMA>(c, x.y, yi[r]);
-                }
-            }
-        }
-    }
-
-    // ---- quantise (limitScale16) and store
-    float2 *out = (float2 *)a.out + ch * a.out_stride;
-    const long n0 = o0 + (long)t * R;
-    const unsigned sh = a.shift;
-    if (n0 + R <= a.n_out && (R % 2) == 0) {
-#pragma unroll
-        for (int r = 0; r < R; r += 2)
-            *(float4 *)(out + n0 + r) = make_float4(q16f(yr[r], sh), q16f(yi[r], sh), q16f(yr[r + 1], sh),
-                                                    q16f(yi[r + 1], sh));
-    } else {
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-            if (n0 + r < a.n_out) out[n0 + r] = make_float2(q16f(yr[r], sh), q16f(yi[r], sh));
-    }
-}
-
-// ============================================================ ci16 tiles
-// complex<int16_t> samples are 4 B, so a 4-sample polyphase group is one
-// 16-B granule.  Lane chunk = R granules; an even R gets one pad granule per
-// chunk (stride R+1 odd), an odd R is conflict-free as is.
-template <int R>
-struct Ci16Geo {
-    static constexpr int PAD = (R % 2 == 0) ? 1 : 0;
-};
-
-// NCO mixer of mixers.h:169-188 on one packed sample
-__device__ __forceinline__ uint32_t mix_sample(uint32_t w, const int16_t *tab, unsigned N, unsigned phi) {
-    unsigned ic = phi + N / 4;  // (phi + N/4) % N with phi < N
-    ic = ic >= N ? ic - N : ic;
-    int32_t lr = tab[ic], li = tab[phi];
-    int32_t ar = sext16(w), ai = sext16_hi(w);
-    int32_t r = ar * lr - ai * li;   // |.| < 2^31: |T| <= 16383
-    int32_t i = ai * lr + li * ar;
-    return pack16(limit16(r, 14), limit16(i, 14));
-}
-
-template <int NT, int R, int BLOCK, bool MIX>
-__global__ __launch_bounds__(BLOCK) void decim_tile_ci16(DecimLaunch a, TapsI taps) {
-    constexpr int NQ = (NT + 3) / 4;
-    constexpr int TO = BLOCK * R;
-    constexpr int TG = TO + NQ;                 // granules of 4 samples
-    constexpr int PAD = Ci16Geo<R>::PAD;
-    constexpr int PR = R;
-    constexpr int KPAD = PAD ? ceildiv(NQ, PR) : 0;
-    constexpr int LG = TG + (PAD ? (TG + KPAD * PR) / PR + 1 : 0);
-    constexpr int PER = ceildiv(TG, BLOCK);
-    constexpr int TABMAX = MIX ? 4096 : 1;
-    __shared__ uint4 lds[LG];
-    __shared__ int16_t tab[TABMAX];
-
-    const int ch = blockIdx.y;
-    const uint32_t *in = (const uint32_t *)a.in + ch * a.in_stride;
-    const uint32_t *hist = (const uint32_t *)a.hist_in[ch];
-    const long n_in = a.n_in;
-    const int H = NT - 1;
-    const long tile = xcd_tile(blockIdx.x, gridDim.x);
-    const long o0 = tile * TO;
-    const long b0 = 4 * o0 - 4 * NQ;
-    const int t = threadIdx.x;
-    const unsigned N = a.mix_N;
-
-    if constexpr (MIX) {
-        for (int i = t; i < (int)N; i += BLOCK) tab[i] = a.mix_table[i];
-        __syncthreads();
-    }
-    // phase of sample idx: (phi0 + idx*freq) mod N (any sign of idx; negative
-    // indices are history and never mixed, but keep the recurrence consistent)
-    auto phase_of = [&](long idx) -> unsigned {
-        long m = idx % (long)N;
-        m = m < 0 ? m + N : m;
-        return (unsigned)(((unsigned long)a.mix_phase0 + (unsigned long)m * a.mix_freq) % N);
-    };
-    auto adv = [&](unsigned ph, unsigned d) -> unsigned {  // (ph + d) mod N, ph,d < N
-        ph += d;
-        return ph >= N ? ph - N : ph;
-    };
-    const unsigned fstep = MIX ? (unsigned)(((unsigned long)(4 * BLOCK) % N) * a.mix_freq % N) : 0;
-    unsigned ph_t = MIX ? phase_of(b0 + 4 * (long)t) : 0;  // phase of this thread's first staged sample
-
-    if (tile == 0) {  // new history = last H samples of (history ++ mixed input)
-        uint32_t *ho = (uint32_t *)a.hist_out[ch];
-        for (int k = t; k < H; k += BLOCK) {
-            long idx = n_in - H + k;
-            uint32_t w = idx >= 0 ? in[idx] : hist[H + idx];
-            if constexpr (MIX)
-                if (idx >= 0) w = mix_sample(w, tab, N, phase_of(idx));
-            ho[k] = w;
-        }
-    }
-
-    uint4 v[PER];
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int g = t + i * BLOCK;
-        const long s = b0 + 4 * (long)g;
-        if (g < TG) {
-            if (s >= 0 && s + 3 < n_in) {
-                v[i] = *(const uint4 *)(in + s);
-                if constexpr (MIX) {
-                    unsigned ph = ph_t;
-                    v[i].x = mix_sample(v[i].x, tab, N, ph); ph = adv(ph, a.mix_freq);
-                    v[i].y = mix_sample(v[i].y, tab, N, ph); ph = adv(ph, a.mix_freq);
-                    v[i].z = mix_sample(v[i].z, tab, N, ph); ph = adv(ph, a.mix_freq);
-                    v[i].w = mix_sample(v[i].w, tab, N, ph);
-                }
-            } else {
-                uint32_t w[4];
-                unsigned ph = ph_t;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    long idx = s + j;
-                    w[j] = fetch(in, hist, idx, n_in, H);
-                    if constexpr (MIX)
-                        if (idx >= 0 && idx < n_in) w[j] = mix_sample(w[j], tab, N, ph);
-                    if constexpr (MIX) ph = adv(ph, a.mix_freq);
-                }
-                v[i] = make_uint4(w[0], w[1], w[2], w[3]);
-            }
-        }
-        if constexpr (MIX) ph_t = adv(ph_t, fstep);
-    }
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int g = t + i * BLOCK;
-        if (g < TG) {
-            int lg = PAD ? g + (g - NQ + KPAD * PR) / PR : g;
-            lds[lg] = v[i];
-        }
-    }
-    __syncthreads();
-
-    const int Bt = PAD ? NQ + KPAD + (PR + 1) * t : NQ + PR * t;
-    int32_t Xr[4 * (NQ + R)], Xi[4 * (NQ + R)];
-    int32_t yr[R], yi[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) yr[r] = yi[r] = 0;
-    auto load_group = [&](int e) {
-        const uint4 g = lds[Bt + e + (PAD ? floordiv(e, PR) : 0)];
-        const int o = 4 * e + 4 * NQ;
-        Xr[o + 0] = sext16(g.x); Xi[o + 0] = sext16_hi(g.x);
-        Xr[o + 1] = sext16(g.y); Xi[o + 1] = sext16_hi(g.y);
-        Xr[o + 2] = sext16(g.z); Xi[o + 2] = sext16_hi(g.z);
-        Xr[o + 3] = sext16(g.w); Xi[o + 3] = sext16_hi(g.w);
-    };
-#pragma unroll
-    for (int e = -1; e < R; ++e) load_group(e);
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        if (q + 1 < NQ) load_group(-q - 2);
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            const int k = 4 * q + p;
-            if (k < NT) {
-                const int32_t c = taps.c[k];
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const int o = 4 * (r - q) - p + 4 * NQ;
-                    yr[r] += __mul24(c, Xr[o]);  // |c| < 2^23, |x| < 2^15: v_mad_i32_i24
-                    yi[r] += __mul24(c, Xi[o]);
-                }
-            }
-        }
-    }
-    uint32_t *out = (uint32_t *)a.out + ch * a.out_stride;
-    const long n0 = o0 + (long)t * R;
-    const unsigned sh = a.shift;
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-        if (n0 + r < a.n_out) out[n0 + r] = pack16(limit16(yr[r], sh), limit16(yi[r], sh));
-}
 
 // ============================================================== dispatch
 namespace {
-constexpr int kCfR = 8, kCfBlock = 256;
+// cf32 tiles: 4 outputs per lane, 256 lanes -> 4096 input samples per tile,
+// 38 KB LDS and 124 VGPRs = 4 resident workgroups (16 waves) per CU; the
+// persistent grid is 2x the resident capacity (measured best on MI355X:
+// scripts/tune, profiles/).
+constexpr int kCfR = 4, kCfBlock = 256, kCfGridCap = 2048;
 constexpr int kCiR = 7, kCiBlock = 256;
 
 template <int NT>
-int launch_cf32(const DecimLaunch &L, const TapsF &T, int channels, bool fma, hipStream_t s) {
+int launch_cf32(DecimLaunch L, int channels, bool fma, hipStream_t s) {
     constexpr int TO = kCfBlock * kCfR;
-    long tiles = (L.n_out + TO - 1) / TO;
-    dim3 grid((unsigned)tiles, channels);
+    L.ntiles = (L.n_out + TO - 1) / TO;
+    dim3 grid((unsigned)std::min<long>(L.ntiles, kCfGridCap), channels);
     if (fma)
-        hipLaunchKernelGGL((decim_tile_cf32<NT, kCfR, kCfBlock, true>), grid, dim3(kCfBlock), 0, s, L, T);
+        hipLaunchKernelGGL((decim_stream_cf32<NT, kCfR, kCfBlock, true, 4>), grid, dim3(kCfBlock), 0, s, L);
     else
-        hipLaunchKernelGGL((decim_tile_cf32<NT, kCfR, kCfBlock, false>), grid, dim3(kCfBlock), 0, s, L, T);
+        hipLaunchKernelGGL((decim_stream_cf32<NT, kCfR, kCfBlock, false, 4>), grid, dim3(kCfBlock), 0, s, L);
     return SRCDSP_OK;
 }
-
 template <int NT>
-int launch_ci16(const DecimLaunch &L, const TapsI &T, int channels, bool mixed, hipStream_t s) {
+int launch_ci16(const DecimLaunch &L, int channels, bool mixed, hipStream_t s) {
     constexpr int TO = kCiBlock * kCiR;
     long tiles = (L.n_out + TO - 1) / TO;
     dim3 grid((unsigned)tiles, channels);
     if (mixed)
-        hipLaunchKernelGGL((decim_tile_ci16<NT, kCiR, kCiBlock, true>), grid, dim3(kCiBlock), 0, s, L, T);
+        hipLaunchKernelGGL((decim_tile_ci16<NT, kCiR, kCiBlock, true>), grid, dim3(kCiBlock), 0, s, L);
     else
-        hipLaunchKernelGGL((decim_tile_ci16<NT, kCiR, kCiBlock, false>), grid, dim3(kCiBlock), 0, s, L, T);
+        hipLaunchKernelGGL((decim_tile_ci16<NT, kCiR, kCiBlock, false>), grid, dim3(kCiBlock), 0, s, L);
     return SRCDSP_OK;
 }
 
@@ -444,13 +85,9 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
     bool al = aligned16(L.in) && ((L.in_stride * kv_in_bytes(f.kv)) % 16 == 0);
     int rc = SRCDSP_OK;
     if (f.M == 4 && f.kv == KV_CF32 && al && (f.ntaps == 127 || f.ntaps == 128)) {
-        TapsF T{};
-        memcpy(T.c, f.h_coef.data(), 4 * (size_t)f.ntaps);
-        rc = f.ntaps == 127 ? launch_cf32<127>(L, T, channels, fma, s) : launch_cf32<128>(L, T, channels, fma, s);
+        rc = f.ntaps == 127 ? launch_cf32<127>(L, channels, fma, s) : launch_cf32<128>(L, channels, fma, s);
     } else if (f.M == 4 && f.kv == KV_CI16_I32 && f.coef_fits_i24 && al && (f.ntaps == 127 || f.ntaps == 128)) {
-        TapsI T{};
-        memcpy(T.c, f.h_coef.data(), 4 * (size_t)f.ntaps);
-        rc = f.ntaps == 127 ? launch_ci16<127>(L, T, channels, mixed, s) : launch_ci16<128>(L, T, channels, mixed, s);
+        rc = f.ntaps == 127 ? launch_ci16<127>(L, channels, mixed, s) : launch_ci16<128>(L, channels, mixed, s);
     } else {
         if (mixed) {
             set_error("mixer->decimator fusion needs variant 1, M=4, 127/128 taps |c|<2^23, 16-B aligned input");
