@@ -34,6 +34,51 @@ __global__ __launch_bounds__(256) void fma_rate(float *out, int iters, float c0)
     out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+// ---- pure streaming probe: read 8 B/sample (dwordx4), write 2 B/sample (1 of 4)
+__global__ __launch_bounds__(256) void stream_probe(const float4 *in, float4 *out, long n16) {
+    // n16 = input granules; each lane reads 4 consecutive granules (8 samples) and writes
+    // one granule (2 samples) -> 4:1 like the decimator
+    long stride = (long)gridDim.x * blockDim.x;
+    for (long k = (long)blockIdx.x * blockDim.x + threadIdx.x; 4 * k + 3 < n16; k += stride) {
+        float4 a = in[4 * k], b = in[4 * k + 1], c = in[4 * k + 2], d = in[4 * k + 3];
+        out[k] = make_float4(a.x + b.y, a.z + c.w, b.x + d.y, c.z + d.w);
+    }
+}
+// coalesced variant: every load instruction reads 1 KiB contiguous per wave,
+// 4 loads in flight per lane, 1 coalesced store per 4 loads
+__global__ __launch_bounds__(256) void stream_probe2(const float4 *in, float4 *out, long n16) {
+    const long nth = (long)gridDim.x * blockDim.x;
+    const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    for (long base = 0; base + 4 * nth <= n16; base += 4 * nth) {
+        float4 a = in[base + tid], b = in[base + nth + tid], c = in[base + 2 * nth + tid], d = in[base + 3 * nth + tid];
+        out[base / 4 + tid] = make_float4(a.x + b.y, a.z + c.w, b.x + d.y, c.z + d.w);
+    }
+}
+// read-only ceiling
+__global__ __launch_bounds__(256) void read_probe(const float4 *in, float *out, long n16) {
+    const long nth = (long)gridDim.x * blockDim.x;
+    float acc = 0;
+    for (long k = (long)blockIdx.x * blockDim.x + threadIdx.x; k < n16; k += nth) {
+        float4 a = in[k];
+        acc += a.x + a.y + a.z + a.w;
+    }
+    if (acc == 12345.678f) out[0] = acc;
+}
+extern "C" int tune_stream_probe2(int mode, int blocks, const void *in, void *out, long n_samples, void *stream) {
+    if (mode == 0)
+        hipLaunchKernelGGL(stream_probe2, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const float4 *)in,
+                           (float4 *)out, n_samples / 2);
+    else
+        hipLaunchKernelGGL(read_probe, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const float4 *)in,
+                           (float *)out, n_samples / 2);
+    return hipGetLastError();
+}
+extern "C" int tune_stream_probe(int blocks, const void *in, void *out, long n_samples, void *stream) {
+    hipLaunchKernelGGL(stream_probe, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const float4 *)in,
+                       (float4 *)out, n_samples / 2);
+    return hipGetLastError();
+}
+
 extern "C" int tune_fma_rate(int mode, int blocks, int iters, float *out, void *stream) {
     if (mode == 0)
         hipLaunchKernelGGL(fma_rate<0>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, out, iters, 1.0f);
@@ -66,6 +111,23 @@ extern "C" int tune_decim(int variant, int grid, const float *d_coef, const void
     case 5: L.ntiles = tiles(128 * 8); return launch(decim_stream_cf32<127, 8, 128, true>, grid, 128, L, s);
     case 6: L.ntiles = tiles(64 * 8); return launch(decim_stream_cf32<127, 8, 64, true>, grid, 64, L, s);
     case 7: L.ntiles = tiles(256 * 6); return launch(decim_stream_cf32<127, 6, 256, true>, grid, 256, L, s);
+    // v2: buffer loads + shift-0 quantiser
+    case 10: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, false>, grid, 256, L, s);
+    case 11: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true>, grid, 256, L, s);
+    case 12: L.ntiles = tiles(128 * 4); return launch(decim_stream2_cf32<127, 4, 128, true, 4, true>, grid, 128, L, s);
+    case 13: L.ntiles = tiles(64 * 4); return launch(decim_stream2_cf32<127, 4, 64, true, 4, true>, grid, 64, L, s);
+    case 14: L.ntiles = tiles(64 * 8); return launch(decim_stream2_cf32<127, 8, 64, true, 2, true>, grid, 64, L, s);
+    case 15: L.ntiles = tiles(128 * 6); return launch(decim_stream2_cf32<127, 6, 128, true, 3, true>, grid, 128, L, s);
+    case 16: L.ntiles = tiles(64 * 6); return launch(decim_stream2_cf32<127, 6, 64, true, 3, true>, grid, 64, L, s);
+    case 20: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 1>, grid, 256, L, s);
+    case 21: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 2>, grid, 256, L, s);
+    case 22: L.ntiles = tiles(64 * 8); return launch(decim_stream2_cf32<127, 8, 64, true, 2, true, 1>, grid, 64, L, s);
+    case 23: L.ntiles = tiles(64 * 8); return launch(decim_stream2_cf32<127, 8, 64, true, 2, true, 2>, grid, 64, L, s);
+    case 30: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 0, true, false>, grid, 256, L, s);
+    case 31: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 0, false, true>, grid, 256, L, s);
+    case 32: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 0, true, true>, grid, 256, L, s);
+    case 33: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 1, true, true>, grid, 256, L, s);
+    case 24: L.ntiles = tiles(128 * 8); return launch(decim_stream2_cf32<127, 8, 128, true, 2, true>, grid, 128, L, s);
     default: return -1;
     }
 }

@@ -3,6 +3,7 @@
 (scripts/tune/libtune.so; not part of the product).  Prints a table."""
 import ctypes as C
 import os
+import time
 import sys
 
 import numpy as np
@@ -37,7 +38,7 @@ def main():
     out = torch.empty(256 * 256 * 16, device="cuda")
     iters = 4000
     print("FMA issue rate (16 chains/lane):")
-    for mode in (0, 1):
+    for mode in ((0, 1) if os.environ.get("TUNE_FMA") else ()):
         for wps in (1, 2, 4, 8):
             blocks = 256 * wps  # 256-thread blocks: 4 waves = 1 per SIMD
             fn = lambda: lib.tune_fma_rate(mode, blocks, iters, C.c_void_p(out.data_ptr()), stream)
@@ -57,14 +58,24 @@ def main():
     c = hamming_sinc(127)
     cdev = torch.from_numpy(c).cuda()
     S.FilterDnsamplingFir(c, 4).step(x, ref)
-    variants = [(0, 0, "tile R8 B256"), (1, 0, "tile R4 B256"), (2, 0, "tile R8 B128"),
-                (3, 256, "stream R8 B256 g256"), (3, 512, "stream R8 B256 g512"),
-                (4, 512, "stream R4 B256 g512"), (4, 1024, "stream R4 B256 g1024"), (4, 2048, "stream R4 B256 g2048"),
-                (5, 512, "stream R8 B128 g512"), (5, 1024, "stream R8 B128 g1024"),
-                (6, 1024, "stream R8 B64 g1024"), (6, 2048, "stream R8 B64 g2048"),
-                (7, 512, "stream R6 B256 g512"), (7, 768, "stream R6 B256 g768")]
+    lib.tune_stream_probe.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_long, C.c_void_p]
+    for blocks in (1024, 2048, 4096, 8192):
+        fn = lambda: lib.tune_stream_probe(blocks, C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), L, stream)
+        fn()
+        med, mn = timeit(fn, 10)
+        print(f"  streaming ceiling probe (8 B in / 2 B out per sample), {blocks} blocks: {mn:.4f} ms "
+              f"-> {10 * L / (mn * 1e-3) / 1e9:.1f} GB/s")
+    lib.tune_stream_probe2.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_long, C.c_void_p]
+    for mode, label, bps in ((0, "coalesced 4:1 stream (10 B/sample)", 10), (1, "read-only stream (8 B/sample)", 8)):
+        for blocks in (2048, 4096, 8192, 16384):
+            fn = lambda: lib.tune_stream_probe2(mode, blocks, C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), L,
+                                                stream)
+            fn()
+            med, mn = timeit(fn, 10)
+            print(f"  {label}, {blocks} blocks: {mn:.4f} ms -> {bps * L / (mn * 1e-3) / 1e9:.1f} GB/s")
+    variants = [(11, 2048, "v2 R4 B256 g2048"), (30, 2048, "v2 +nt loads"), (20, 2048, "PROBE mem-only R4 B256")]
     res = {v: [] for v in variants}
-    for rnd in range(5):
+    for rnd in range(int(os.environ.get('TUNE_ROUNDS', '6'))):
         for v in variants:
             fn = lambda: lib.tune_decim(v[0], v[1], C.c_void_p(cdev.data_ptr()), C.c_void_p(x.data_ptr()),
                                         C.c_void_p(y.data_ptr()), L, C.c_void_p(h0.data_ptr()),
@@ -75,15 +86,33 @@ def main():
                 fn()
                 torch.cuda.synchronize()
                 ok = torch.equal(y.view(torch.float32), ref.view(torch.float32))
-                res[v].append(("ok" if ok else "MISMATCH"))
+                res[v].append(("ok" if ok else ("n/a" if "PROBE" in v[2] else "MISMATCH")))
             med, mn = timeit(fn, 5)
             res[v].append(mn)
     print(f"decimator cf32 M=4 127 taps, 2^28 samples (min over rounds):")
     for v in variants:
         tmin = min(t for t in res[v][1:])
         gbs = 10 * L / (tmin * 1e-3) / 1e9
-        print(f"  {v[2]:24s} {res[v][0]:8s} {tmin:.4f} ms  {L / tmin / 1e6:8.1f} Gsamp/s  {gbs:7.1f} GB/s "
+        print(f"  {v[2]:28s} {res[v][0]:8s} {tmin:.4f} ms  {L / tmin / 1e6:8.1f} Gsamp/s  {gbs:7.1f} GB/s "
               f"({gbs / 8000 * 100:.1f}% of 8 TB/s)")
+    sustained(variants, x, y, cdev, h0, h1, stream, L)
+
+
+def sustained(variants, x, y, cdev, h0, h1, stream, L, reps=60):
+    print("sustained back-to-back (60 launches each; median of last 20, first 5):")
+    for v in variants:
+        st = torch.cuda.current_stream()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for i in range(reps):
+            ev[i][0].record(st)
+            lib.tune_decim(v[0], v[1], C.c_void_p(cdev.data_ptr()), C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()),
+                           L, C.c_void_p(h0.data_ptr()), C.c_void_p(h1.data_ptr()), stream)
+            ev[i][1].record(st)
+        torch.cuda.synchronize()
+        t = [a.elapsed_time(b) for a, b in ev]
+        print(f"  {v[2]:28s} first5 {np.median(t[:5]):.4f} ms  last20 {np.median(t[-20:]):.4f} ms "
+              f"-> {10 * L / (np.median(t[-20:]) * 1e-3) / 1e9:7.1f} GB/s")
+        time.sleep(2)
 
 
 if __name__ == "__main__":

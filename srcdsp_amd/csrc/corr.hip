@@ -20,13 +20,19 @@
 #include <vector>
 
 #include "ops.h"
+#include "decim_kernels.h"
 
 namespace srcdsp {
+
+typedef short short2_t __attribute__((ext_vector_type(2)));
 
 struct srcdsp_corr_state {
     unsigned N = 0, S = 1, NS = 0;
     int32_t *d_coef = nullptr;   // conj(pattern), N complex<int32_t> (2N int32)
     std::vector<int32_t> h_coef;
+    uint32_t *d_ptaps = nullptr; // packed int16 pairs for v_dot2: (p.re,p.im),(-p.im,p.re) per tap
+    bool taps16 = false;         // every pattern component fits int16 (always true when the
+                                 // reference's energy assert holds)
     uint32_t *d_hist[2] = {nullptr, nullptr};  // last NS-1 effective samples (packed ci16)
     int cur = 0;
     uint32_t *d_corr = nullptr, *d_en = nullptr;  // per-sample scratch
@@ -90,8 +96,8 @@ __device__ __forceinline__ uint32_t corr_fetch(const uint32_t *in, const uint32_
 constexpr int kCorrBlock = 256;
 
 // one output per lane; the block's window span and the taps are staged in LDS
-__global__ __launch_bounds__(kCorrBlock) void corr_eval(const uint32_t *__restrict__ in, long n,
-                                                        const uint32_t *__restrict__ hist,
+__global__ __launch_bounds__(kCorrBlock) void corr_eval(const uint32_t *__restrict__ in, long n, long i_begin,
+                                                        long i_end, const uint32_t *__restrict__ hist,
                                                         const int32_t *__restrict__ coef, unsigned N, unsigned S,
                                                         unsigned cs, uint32_t *__restrict__ corr_out,
                                                         uint32_t *__restrict__ en_out) {
@@ -100,7 +106,7 @@ __global__ __launch_bounds__(kCorrBlock) void corr_eval(const uint32_t *__restri
     const long span = kCorrBlock + NSm1;  // samples i0-NSm1 .. i0+255
     uint32_t *xs = sm;
     int2 *cs2 = (int2 *)(sm + ((span + 3) & ~3l));
-    const long i0 = (long)blockIdx.x * kCorrBlock;
+    const long i0 = i_begin + (long)blockIdx.x * kCorrBlock;
     for (long k = threadIdx.x; k < span; k += kCorrBlock) {
         long j = i0 - NSm1 + k;
         xs[k] = j < n ? corr_fetch(in, hist, j, NSm1) : 0u;
@@ -108,7 +114,7 @@ __global__ __launch_bounds__(kCorrBlock) void corr_eval(const uint32_t *__restri
     for (unsigned m = threadIdx.x; m < N; m += kCorrBlock) cs2[m] = make_int2(coef[2 * m], coef[2 * m + 1]);
     __syncthreads();
     const long i = i0 + threadIdx.x;
-    if (i >= n) return;
+    if (i >= i_end) return;
     uint32_t tr = 0, ti = 0, e = 0;
     // window sample of tap m: x[i - (N-1-m) S]  ->  xs[threadIdx.x + (S-1) + m S]
     const uint32_t *xw = xs + threadIdx.x + (S - 1);
@@ -126,9 +132,117 @@ __global__ __launch_bounds__(kCorrBlock) void corr_eval(const uint32_t *__restri
     en_out[i] = e >> ((unsigned)((int)cs / 2) & 31u);                                // :245
 }
 
-__global__ void corr_detect(const uint32_t *__restrict__ corr, const uint32_t *__restrict__ en, long n,
-                            uint32_t c_prev0, uint32_t c_prev1, uint32_t e_prev0, unsigned *best) {
-    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+// ------------------------------------------------- S == 1 register-tiled eval
+// For stride 1 the correlation is a complex FIR over the last N samples:
+//   C_i = sum_m x[i-(N-1)+m] * conj(p[m]).
+// With packed complex<int16_t> words both real products of a tap are one
+// v_dot2_i32_i16 (int16 x int16 -> int32, wrap-around accumulate, as the
+// reference's complex<int32_t> arithmetic):
+//   Re = dot2(x, (p.re, p.im)),  Im = dot2(x, (-p.im, p.re)).
+// Each lane owns CR consecutive outputs and slides a register window over the
+// taps (16 taps per chunk: CR+15 window words, 4 new ds_read_b128 per chunk for
+// 2*16*CR dot2).  Window energy: direct sum for the lane's first output
+// (one dot2(x,x) per tap), then E_{i+1} = E_i + |x_{i+1}|^2 - |x_{i+1-N}|^2.
+// Taps (2N packed words) are scalar loads through a constant view.  The LDS
+// image gets one 16-B pad per lane chunk (CR words), so the 16 lanes of a
+// ds_read_b128 group touch 16 distinct bank slots.
+constexpr int kCR = 16;       // outputs per lane
+constexpr int kCBlock = 256;  // lanes per workgroup
+
+__global__ __launch_bounds__(kCBlock) void corr_eval_s1(const uint32_t *__restrict__ in, long n, long i_begin,
+                                                         long i_end, const uint32_t *__restrict__ hist,
+                                                         const uint32_t *__restrict__ ptaps, int N, unsigned cs,
+                                                         uint32_t *__restrict__ corr_out,
+                                                         uint32_t *__restrict__ en_out) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t xs[];
+    constexpr int TO = kCBlock * kCR;
+    const long i0 = i_begin + (long)blockIdx.x * TO;  // first output of the tile
+    const long base = i0 - (N - 1);                   // first sample the tile needs
+    const int span = TO + N - 1;
+    // LDS word of tile sample l (l = sample - base): lp = l + 1 (aligns the lane
+    // windows' new words to 16 B), one 4-word pad per kCR = 16 words, i.e.
+    // 20-word chunks of which the last 4 are padding
+    static_assert(kCR == 16, "LDS chunk geometry assumes 16 outputs per lane");
+    auto lw = [&](int l) { int lp = l + 1; return lp + 4 * (lp / kCR); };
+    for (int l = threadIdx.x; l < span; l += kCBlock) {
+        long j = base + l;
+        uint32_t w = 0;
+        if (j < n) w = j >= 0 ? in[j] : (j + (N - 1) >= 0 ? hist[j + (N - 1)] : 0u);
+        xs[lw(l)] = w;
+    }
+    __syncthreads();
+    const int t = threadIdx.x;
+    // lane window W[j] = sample base + t*kCR + j  ->  LDS lw(t*kCR + j)
+    int32_t ar[kCR], ai[kCR];
+#pragma unroll
+    for (int r = 0; r < kCR; ++r) ar[r] = ai[r] = 0;
+    int32_t e0 = 0;
+    const int lb = t * kCR;  // lane base in sample units
+    // Window words j = 0..30 of a 16-tap chunk: j < 15 were loaded by the
+    // previous chunk (its words 16..30), j >= 15 are the chunk's 16 new words.
+    // Two register sets alternate roles (unrolled by 2), so sliding the window
+    // costs no moves.
+    uint32_t A[kCR + 15], B[kCR + 15];
+#pragma unroll
+    for (int j = 0; j < kCR - 1; ++j) B[16 + j] = xs[lw(lb + j)];
+    ConstPtr<uint32_t> tp = const_view<uint32_t>(ptaps);
+    auto chunk = [&](int m0, uint32_t(&cur)[kCR + 15], const uint32_t(&prev)[kCR + 15]) {
+        asm volatile("" : "+s"(tp));
+        uint32_t pw[32];  // this chunk's 16 taps (2 x s_load_dwordx16)
+#pragma unroll
+        for (int k = 0; k < 32; ++k) pw[k] = tp[2 * m0 + k];
+        // new words: the whole 16-word LDS chunk t+1+m0/16 = uint4 slots 5(t+1+m0/16)..+3
+        const uint4 *src = (const uint4 *)xs + 5 * (t + 1 + (m0 >> 4));
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const uint4 q = src[g];
+            cur[kCR - 1 + 4 * g + 0] = q.x;
+            cur[kCR - 1 + 4 * g + 1] = q.y;
+            cur[kCR - 1 + 4 * g + 2] = q.z;
+            cur[kCR - 1 + 4 * g + 3] = q.w;
+        }
+        auto word = [&](int j) { return j < kCR - 1 ? prev[16 + j] : cur[j]; };
+#pragma unroll
+        for (int mm = 0; mm < 16; ++mm) {
+            const uint32_t p0 = pw[2 * mm], p1 = pw[2 * mm + 1];
+            const short2_t x0 = __builtin_bit_cast(short2_t, word(mm));
+            e0 = __builtin_amdgcn_sdot2(x0, x0, e0, false);
+#pragma unroll
+            for (int r = 0; r < kCR; ++r) {
+                const short2_t x = __builtin_bit_cast(short2_t, word(mm + r));
+                ar[r] = __builtin_amdgcn_sdot2(x, __builtin_bit_cast(short2_t, p0), ar[r], false);
+                ai[r] = __builtin_amdgcn_sdot2(x, __builtin_bit_cast(short2_t, p1), ai[r], false);
+            }
+        }
+    };
+    int m0 = 0;
+    for (; m0 + 32 <= N; m0 += 32) {  // N % 16 == 0 (host-checked)
+        chunk(m0, A, B);
+        chunk(m0 + 16, B, A);
+    }
+    if (m0 < N) chunk(m0, A, B);
+    // outputs, energies (sliding) and stores
+    uint32_t e = (uint32_t)e0;
+    for (int r = 0; r < kCR; ++r) {
+        const long i = i0 + lb + r;
+        if (r > 0) {  // E_{i} = E_{i-1} + |x_i|^2 - |x_{i-N}|^2
+            const uint32_t xn = xs[lw(lb + r + N - 1)], xo = xs[lw(lb + r - 1)];
+            const short2_t a = __builtin_bit_cast(short2_t, xn), b = __builtin_bit_cast(short2_t, xo);
+            e += (uint32_t)__builtin_amdgcn_sdot2(a, a, 0, false) - (uint32_t)__builtin_amdgcn_sdot2(b, b, 0, false);
+        }
+        if (i < i_end) {
+            const int32_t sr = ar[r] >> (cs & 31u), si = ai[r] >> (cs & 31u);
+            const int32_t qr = sr >> 2, qi = si >> 2;
+            corr_out[i] = (uint32_t)qr * (uint32_t)qr + (uint32_t)qi * (uint32_t)qi;
+            en_out[i] = e >> ((unsigned)((int)cs / 2) & 31u);
+        }
+    }
+}
+
+__global__ void corr_detect(const uint32_t *__restrict__ corr, const uint32_t *__restrict__ en, long i_begin,
+                            long i_end, uint32_t c_prev0, uint32_t c_prev1, uint32_t e_prev0, unsigned *best) {
+    for (long i = i_begin + (long)blockIdx.x * blockDim.x + threadIdx.x; i < i_end;
+         i += (long)gridDim.x * blockDim.x) {
         const uint32_t c0 = corr[i];
         const uint32_t c1 = i >= 1 ? corr[i - 1] : c_prev0;
         const uint32_t c2 = i >= 2 ? corr[i - 2] : (i == 1 ? c_prev0 : c_prev1);
@@ -172,20 +286,35 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
     const long NSm1 = (long)c.NS - 1;
     const uint32_t *hist = c.d_hist[c.cur];
     const unsigned cs = (unsigned)c.coeff_scaling;
-    const size_t smem = 4 * (size_t)((kCorrBlock + NSm1 + 3) & ~3l) + 8 * (size_t)c.N;
-    const long blocks = (n + kCorrBlock - 1) / kCorrBlock;
-    hipLaunchKernelGGL(corr_eval, dim3((unsigned)blocks), dim3(kCorrBlock), smem, s, d_in, n, hist, c.d_coef, c.N,
-                       c.S, cs, c.d_corr, c.d_en);
-    SRCDSP_HIP_TRY(hipGetLastError());
+    const bool fast = c.S == 1 && c.N % 16 == 0 && c.taps16;
+    // The reference stops at the first detection (break, correlators.h:291):
+    // scan in segments and stop after the first segment holding one.
+    const long seg = std::max<long>(1L << 23, (n + 7) / 8);
     const unsigned none = 0xffffffffu;
-    SRCDSP_HIP_TRY(hipMemcpyAsync(c.d_best, &none, 4, hipMemcpyHostToDevice, s));
-    const int db = (int)std::max<long>(1, std::min<long>((n + 255) / 256, 4096));
-    hipLaunchKernelGGL(corr_detect, dim3(db), dim3(256), 0, s, c.d_corr, c.d_en, n, c.corr[0], c.corr[1],
-                       c.energy[0], c.d_best);
-    SRCDSP_HIP_TRY(hipGetLastError());
     unsigned best = none;
-    SRCDSP_HIP_TRY(hipMemcpyAsync(&best, c.d_best, 4, hipMemcpyDeviceToHost, s));
-    SRCDSP_HIP_TRY(hipStreamSynchronize(s));
+    for (long sb = 0; sb < n && best == none; sb += seg) {
+        const long se = std::min(n, sb + seg);
+        if (fast) {
+            constexpr long TO = (long)kCBlock * kCR;
+            const long blocks = (se - sb + TO - 1) / TO;
+            const size_t smem = 4 * (size_t)(((TO + c.N + 1) / kCR + 2) * (kCR + 4));
+            hipLaunchKernelGGL(corr_eval_s1, dim3((unsigned)blocks), dim3(kCBlock), smem, s, d_in, n, sb, se, hist,
+                               c.d_ptaps, (int)c.N, cs, c.d_corr, c.d_en);
+        } else {
+            const size_t smem = 4 * (size_t)((kCorrBlock + NSm1 + 3) & ~3l) + 8 * (size_t)c.N;
+            const long blocks = (se - sb + kCorrBlock - 1) / kCorrBlock;
+            hipLaunchKernelGGL(corr_eval, dim3((unsigned)blocks), dim3(kCorrBlock), smem, s, d_in, n, sb, se, hist,
+                               c.d_coef, c.N, c.S, cs, c.d_corr, c.d_en);
+        }
+        SRCDSP_HIP_TRY(hipGetLastError());
+        SRCDSP_HIP_TRY(hipMemcpyAsync(c.d_best, &none, 4, hipMemcpyHostToDevice, s));
+        const int db = (int)std::max<long>(1, std::min<long>((se - sb + 255) / 256, 4096));
+        hipLaunchKernelGGL(corr_detect, dim3(db), dim3(256), 0, s, c.d_corr, c.d_en, sb, se, c.corr[0], c.corr[1],
+                           c.energy[0], c.d_best);
+        SRCDSP_HIP_TRY(hipGetLastError());
+        SRCDSP_HIP_TRY(hipMemcpyAsync(&best, c.d_best, 4, hipMemcpyDeviceToHost, s));
+        SRCDSP_HIP_TRY(hipStreamSynchronize(s));
+    }
 
     const bool hit = best != none;
     const long last = hit ? (long)best : n - 1;  // last processed sample
@@ -278,6 +407,7 @@ SRCDSP_API int srcdsp_corr_create(srcdsp_corr_t *out, unsigned N, unsigned S) {
     }
     const size_t hb = 4 * (size_t)std::max(1u, c.NS - 1);
     if (hipMalloc(&c.d_coef, 8 * (size_t)N) != hipSuccess || hipMemset(c.d_coef, 0, 8 * (size_t)N) != hipSuccess ||
+        hipMalloc(&c.d_ptaps, 8 * (size_t)N) != hipSuccess || hipMemset(c.d_ptaps, 0, 8 * (size_t)N) != hipSuccess ||
         hipMalloc(&c.d_hist[0], hb) != hipSuccess || hipMalloc(&c.d_hist[1], hb) != hipSuccess ||
         hipMemset(c.d_hist[0], 0, hb) != hipSuccess || hipMalloc(&c.d_best, 4) != hipSuccess) {
         set_error("corr_create: device allocation failed");
@@ -292,7 +422,7 @@ SRCDSP_API int srcdsp_corr_destroy(srcdsp_corr_t h) {
     if (!h) return SRCDSP_OK;
     srcdsp_corr_state &c = h->c;
     (void)c.order.sync();
-    for (void *p : {(void *)c.d_coef, (void *)c.d_hist[0], (void *)c.d_hist[1], (void *)c.d_corr, (void *)c.d_en,
+    for (void *p : {(void *)c.d_coef, (void *)c.d_ptaps, (void *)c.d_hist[0], (void *)c.d_hist[1], (void *)c.d_corr, (void *)c.d_en,
                     (void *)c.d_best})
         if (p) (void)hipFree(p);
     c.order.destroy();
@@ -322,6 +452,15 @@ SRCDSP_API int srcdsp_corr_set_pattern(srcdsp_corr_t h, const int32_t *p, double
     c.threshold_factor = th * std::sqrt((double)c.coeffs_energy);
     c.coeff_scaling = cvt_d2i_x86(std::floor(std::log2(std::sqrt((double)c.coeffs_energy))));
     SRCDSP_HIP_TRY(hipMemcpy(c.d_coef, c.h_coef.data(), 8 * (size_t)c.N, hipMemcpyHostToDevice));
+    c.taps16 = true;
+    std::vector<uint32_t> pk(2 * (size_t)c.N);
+    for (unsigned i = 0; i < c.N; ++i) {
+        const int32_t pr = p[2 * i], pi = p[2 * i + 1];
+        if (pr < -32767 || pr > 32767 || pi < -32767 || pi > 32767) c.taps16 = false;
+        pk[2 * i] = ((uint32_t)pr & 0xffffu) | ((uint32_t)pi << 16);       // Re = x.re*p.re + x.im*p.im
+        pk[2 * i + 1] = ((uint32_t)(-pi) & 0xffffu) | ((uint32_t)pr << 16);  // Im = -x.re*p.im + x.im*p.re
+    }
+    SRCDSP_HIP_TRY(hipMemcpy(c.d_ptaps, pk.data(), 8 * (size_t)c.N, hipMemcpyHostToDevice));
     return SRCDSP_OK;
 }
 

@@ -47,12 +47,18 @@ int launch_cf32(DecimLaunch L, int channels, bool fma, hipStream_t s) {
     constexpr int TO = kCfBlock * kCfR;
     L.ntiles = (L.n_out + TO - 1) / TO;
     dim3 grid((unsigned)std::min<long>(L.ntiles, kCfGridCap), channels);
-    if (fma)
-        hipLaunchKernelGGL((decim_stream_cf32<NT, kCfR, kCfBlock, true, 4>), grid, dim3(kCfBlock), 0, s, L);
+    const bool q0 = (L.shift & 31u) == 0;  // limitScale16 shift 0: the 4-op float quantiser
+    if (fma && q0)
+        hipLaunchKernelGGL((decim_stream2_cf32<NT, kCfR, kCfBlock, true, 4, true>), grid, dim3(kCfBlock), 0, s, L);
+    else if (fma)
+        hipLaunchKernelGGL((decim_stream2_cf32<NT, kCfR, kCfBlock, true, 4, false>), grid, dim3(kCfBlock), 0, s, L);
+    else if (q0)
+        hipLaunchKernelGGL((decim_stream2_cf32<NT, kCfR, kCfBlock, false, 3, true>), grid, dim3(kCfBlock), 0, s, L);
     else
-        hipLaunchKernelGGL((decim_stream_cf32<NT, kCfR, kCfBlock, false, 4>), grid, dim3(kCfBlock), 0, s, L);
+        hipLaunchKernelGGL((decim_stream2_cf32<NT, kCfR, kCfBlock, false, 3, false>), grid, dim3(kCfBlock), 0, s, L);
     return SRCDSP_OK;
 }
+
 template <int NT>
 int launch_ci16(const DecimLaunch &L, int channels, bool mixed, hipStream_t s) {
     constexpr int TO = kCiBlock * kCiR;

@@ -500,3 +500,167 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream_cf32(DecimLaunch a) 
 }
 
 }  // namespace srcdsp
+namespace srcdsp {
+
+// limitScale16 of a float accumulator when (coeffScaling - leftShift) & 31 == 0:
+// trunc, clamp to +-32767, and 0 for |y| >= 2^31 or NaN (x86 cvttss2si gives
+// INT_MIN there, which limitScale16 passes through and int16 truncates to 0).
+// 4 VALU ops instead of the integer path's ~8; identical results.
+__device__ __forceinline__ float q16f_shift0(float y) {
+    const float t = __builtin_fminf(__builtin_fmaxf(__builtin_truncf(y), -32767.0f), 32767.0f);
+    return __builtin_fabsf(y) < 2147483648.0f ? t : 0.0f;
+}
+
+// Persistent cf32 decimator, v2: as decim_stream_cf32, plus
+//  * buffer_load_dwordx4 staging through a per-tile buffer descriptor
+//    (32-bit lane offsets, hardware range check returns 0 past the input end,
+//    so the tail needs no per-lane compare) -- fewer VALU ops per load;
+//  * Q0: the shift-0 quantiser above (host selects it when shift & 31 == 0).
+// PROBE (tuning only): 0 = real kernel; 1 = memory path only (no FMA loop);
+// 2 = compute path only (every tile reads the same L2-resident input span)
+// NTL: non-temporal (streaming) input loads; OST: outputs staged through LDS
+// so each store instruction writes whole contiguous lines.
+template <int NT, int R, int BLOCK, bool FMA, int MINW, bool Q0, int PROBE = 0, bool NTL = false, bool OST = false>
+__global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a) {
+    constexpr int NQ = (NT + 3) / 4;
+    constexpr int TO = BLOCK * R;
+    constexpr int TG = 2 * TO + 2 * NQ;
+    constexpr int PR = 2 * R;
+    constexpr int KPAD = ceildiv(2 * NQ, PR);
+    constexpr int LG = TG + (TG + KPAD * PR) / PR + 1;
+    constexpr int PER = ceildiv(TG, BLOCK);
+    __shared__ float4 lds[LG];
+
+    const int ch = blockIdx.y;
+    const float2 *in = (const float2 *)a.in + ch * a.in_stride;
+    const float2 *hist = (const float2 *)a.hist_in[ch];
+    float2 *out = (float2 *)a.out + ch * a.out_stride;
+    const long n_in = a.n_in;
+    const int H = NT - 1;
+    const int t = threadIdx.x;
+    const long nb = gridDim.x;
+    const long b = xcd_tile(blockIdx.x, nb);
+    const long per = a.ntiles / nb, rem = a.ntiles % nb;
+    const long t_begin = b * per + (b < rem ? b : rem);
+    const long t_end = t_begin + per + (b < rem ? 1 : 0);
+    if (t_begin == 0 && t_end > 0) write_history(in, n_in, hist, (float2 *)a.hist_out[ch], H);
+
+    float4 v[PER];
+    // tiles >= 1: one descriptor per tile, 32-bit lane offsets, range-checked
+    auto stage_load = [&](long tile) {
+        if constexpr (PROBE == 2) tile = 1 + (tile & 15);
+        const long b0 = 4 * tile * TO - 4 * NQ;  // >= 0 for tile >= 1
+        const long remb = (n_in - b0) * 8;
+        const unsigned nrec = (unsigned)(remb > 0xfffffff0L ? 0xfffffff0L : (remb < 0 ? 0 : remb));
+        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)(in + b0), 0, nrec, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int g = t + i * BLOCK;
+            if (g < TG) {
+                auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * g, 0, NTL ? 2 : 0);  // aux 2 = nt
+                v[i] = make_float4(__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]),
+                                   __uint_as_float(w[3]));
+            }
+        }
+    };
+    if (t_begin < t_end) {
+        if (t_begin == 0) {  // tile 0: the halo comes from the history
+            const long b0 = -4 * NQ;
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int g = t + i * BLOCK;
+                const long s = b0 + 2 * (long)g;
+                if (g < TG) {
+                    float2 lo = fetch(in, hist, s, n_in, H), hi = fetch(in, hist, s + 1, n_in, H);
+                    v[i] = make_float4(lo.x, lo.y, hi.x, hi.y);
+                }
+            }
+        } else {
+            stage_load(t_begin);
+        }
+    }
+    const int Bt = 2 * NQ + KPAD + (PR + 1) * t;
+    for (long tile = t_begin; tile < t_end; ++tile) {
+        SRCDSP_LDS_BARRIER();
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int g = t + i * BLOCK;
+            if (g < TG) lds[g + (g - 2 * NQ + KPAD * PR) / PR] = v[i];
+        }
+        SRCDSP_LDS_BARRIER();
+        if (tile + 1 < t_end) stage_load(tile + 1);
+
+        ConstPtr<float> tp = const_view<float>(a.coef);
+        asm volatile("" : "+s"(tp));
+        float2 X[4 * (NQ + R)];
+        float yr[R], yi[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) yr[r] = yi[r] = 0.f;
+        auto load_group = [&](int e) {
+            const float4 g0 = lds[Bt + 2 * e + floordiv(2 * e, PR)];
+            const float4 g1 = lds[Bt + 2 * e + 1 + floordiv(2 * e + 1, PR)];
+            X[4 * e + 4 * NQ + 0] = make_float2(g0.x, g0.y);
+            X[4 * e + 4 * NQ + 1] = make_float2(g0.z, g0.w);
+            X[4 * e + 4 * NQ + 2] = make_float2(g1.x, g1.y);
+            X[4 * e + 4 * NQ + 3] = make_float2(g1.z, g1.w);
+        };
+#pragma unroll
+        for (int e = -1; e < R; ++e) load_group(e);
+        if constexpr (PROBE == 1) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) { yr[r] = X[4 * r + 4 * NQ].x; yi[r] = X[4 * r + 4 * NQ].y; }
+        } else
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            if (q + 1 < NQ) load_group(-q - 2);
+            if ((q & 3) == 0) asm volatile("" : "+s"(tp));
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                const int k = 4 * q + p;
+                if (k < NT) {
+                    const float c = tp[k];
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const float2 x = X[4 * (r - q) - p + 4 * NQ];
+                        yr[r] = mac<FMA>(c, x.x, yr[r]);
+                        yi[r] = mac<FMA>(c, x.y, yi[r]);
+                    }
+                }
+            }
+        }
+        const long n0 = tile * TO + (long)t * R;
+        const unsigned sh = a.shift;
+        auto q = [&](float y) { return Q0 ? q16f_shift0(y) : q16f(y, sh); };
+        if constexpr (OST) {
+            // outputs -> LDS (reusing the tile image once every wave is done
+            // reading it) -> 16-B lane-contiguous stores of the whole tile
+            const long o0 = tile * TO;
+            SRCDSP_LDS_BARRIER();
+            float2 *ob = (float2 *)lds;
+#pragma unroll
+            for (int r = 0; r < R; ++r) ob[t * R + r] = make_float2(q(yr[r]), q(yi[r]));
+            SRCDSP_LDS_BARRIER();
+            const float4 *ob4 = (const float4 *)lds;
+            if (o0 + TO <= a.n_out) {
+#pragma unroll
+                for (int i = 0; i < TO / 2 / BLOCK; ++i) {
+                    const int k = t + i * BLOCK;
+                    *(float4 *)(out + o0 + 2 * k) = ob4[k];
+                }
+            } else {
+                for (int k = t; k < TO; k += BLOCK)
+                    if (o0 + k < a.n_out) out[o0 + k] = ob[k];
+            }
+        } else if (n0 + R <= a.n_out && (R % 2) == 0) {
+#pragma unroll
+            for (int r = 0; r < R; r += 2)
+                *(float4 *)(out + n0 + r) = make_float4(q(yr[r]), q(yi[r]), q(yr[r + 1]), q(yi[r + 1]));
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (n0 + r < a.n_out) out[n0 + r] = make_float2(q(yr[r]), q(yi[r]));
+        }
+    }
+}
+
+}  // namespace srcdsp
