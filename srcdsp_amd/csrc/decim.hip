@@ -35,12 +35,19 @@ namespace srcdsp {
 
 // ============================================================== dispatch
 namespace {
+constexpr int kCiR_ = 4, kCiBlock_ = 256;
+}
+// phase advance of the fused mixer per ci16 tile (4 * TO samples)
+unsigned phase_step_tile(unsigned long N, unsigned long fr) {
+    return (unsigned)(((4ul * kCiBlock_ * kCiR_) % N) * fr % N);
+}
+namespace {
 // cf32 tiles: 4 outputs per lane, 256 lanes -> 4096 input samples per tile,
 // 38 KB LDS and 124 VGPRs = 4 resident workgroups (16 waves) per CU; the
 // persistent grid is 2x the resident capacity (measured best on MI355X:
 // scripts/tune, profiles/).
 constexpr int kCfR = 4, kCfBlock = 256, kCfGridCap = 2048;
-constexpr int kCiR = 7, kCiBlock = 256;
+constexpr int kCiR = 4, kCiBlock = 256;
 
 template <int NT>
 int launch_cf32(DecimLaunch L, int channels, bool fma, hipStream_t s) {
@@ -60,14 +67,14 @@ int launch_cf32(DecimLaunch L, int channels, bool fma, hipStream_t s) {
 }
 
 template <int NT>
-int launch_ci16(const DecimLaunch &L, int channels, bool mixed, hipStream_t s) {
+int launch_ci16(DecimLaunch L, int channels, bool mixed, hipStream_t s) {
     constexpr int TO = kCiBlock * kCiR;
-    long tiles = (L.n_out + TO - 1) / TO;
-    dim3 grid((unsigned)tiles, channels);
+    L.ntiles = (L.n_out + TO - 1) / TO;
+    dim3 grid((unsigned)std::min<long>(L.ntiles, kCfGridCap), channels);
     if (mixed)
-        hipLaunchKernelGGL((decim_tile_ci16<NT, kCiR, kCiBlock, true>), grid, dim3(kCiBlock), 0, s, L);
+        hipLaunchKernelGGL((decim_stream_ci16<NT, kCiR, kCiBlock, true, 4>), grid, dim3(kCiBlock), 0, s, L);
     else
-        hipLaunchKernelGGL((decim_tile_ci16<NT, kCiR, kCiBlock, false>), grid, dim3(kCiBlock), 0, s, L);
+        hipLaunchKernelGGL((decim_stream_ci16<NT, kCiR, kCiBlock, false, 4>), grid, dim3(kCiBlock), 0, s, L);
     return SRCDSP_OK;
 }
 
@@ -216,10 +223,21 @@ static int core_step(FirCore &f, const void *d_in, size_t n_in, void *d_out, siz
     L.hist_in[0] = f.d_hist[f.cur];
     L.hist_out[0] = f.d_hist[f.cur ^ 1];
     if (mix) {
+        const unsigned long N = mix->N, fr = (unsigned)mix->freq, phi0 = (unsigned)mix->phi;
+        // phase of sample i: (phi0 + i*fr) mod N, for any sign of i
+        auto phase = [&](long i) {
+            long m = i % (long)N;
+            if (m < 0) m += (long)N;
+            return (unsigned)((phi0 + (unsigned long)m * fr) % N);
+        };
+        constexpr long kNQ = 32;  // taps 127/128: ceil(N/4) polyphase steps
         L.mix_table = mix->d_table;
         L.mix_N = mix->N;
-        L.mix_phase0 = (unsigned)mix->phi;
-        L.mix_freq = (unsigned)mix->freq;
+        L.mix_phase0 = (unsigned)phi0;
+        L.mix_freq = (unsigned)fr;
+        L.mix_phase_tile0 = phase(-4 * kNQ);
+        L.mix_dtile = phase_step_tile(N, fr);
+        L.mix_phase_hist = phase((long)n_in - (f.ntaps - 1));
     }
     rc = decim_launch(f, L, 1, s, mix != nullptr);
     if (rc) return rc;

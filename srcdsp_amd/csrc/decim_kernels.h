@@ -243,143 +243,6 @@ __device__ __forceinline__ uint32_t mix_sample(uint32_t w, const int16_t *tab, u
     return pack16(limit16(r, 14), limit16(i, 14));
 }
 
-template <int NT, int R, int BLOCK, bool MIX>
-__global__ __launch_bounds__(BLOCK) void decim_tile_ci16(DecimLaunch a) {
-    constexpr int NQ = (NT + 3) / 4;
-    constexpr int TO = BLOCK * R;
-    constexpr int TG = TO + NQ;                 // granules of 4 samples
-    constexpr int PAD = Ci16Geo<R>::PAD;
-    constexpr int PR = R;
-    constexpr int KPAD = PAD ? ceildiv(NQ, PR) : 0;
-    constexpr int LG = TG + (PAD ? (TG + KPAD * PR) / PR + 1 : 0);
-    constexpr int PER = ceildiv(TG, BLOCK);
-    constexpr int TABMAX = MIX ? 4096 : 1;
-    __shared__ uint4 lds[LG];
-    __shared__ int16_t tab[TABMAX];
-
-    const int ch = blockIdx.y;
-    const uint32_t *in = (const uint32_t *)a.in + ch * a.in_stride;
-    const uint32_t *hist = (const uint32_t *)a.hist_in[ch];
-    const long n_in = a.n_in;
-    const int H = NT - 1;
-    const long tile = xcd_tile(blockIdx.x, gridDim.x);
-    const long o0 = tile * TO;
-    const long b0 = 4 * o0 - 4 * NQ;
-    const int t = threadIdx.x;
-    const unsigned N = a.mix_N;
-
-    if constexpr (MIX) {
-        for (int i = t; i < (int)N; i += BLOCK) tab[i] = a.mix_table[i];
-        __syncthreads();
-    }
-    // phase of sample idx: (phi0 + idx*freq) mod N (any sign of idx; negative
-    // indices are history and never mixed, but keep the recurrence consistent)
-    auto phase_of = [&](long idx) -> unsigned {
-        long m = idx % (long)N;
-        m = m < 0 ? m + N : m;
-        return (unsigned)(((unsigned long)a.mix_phase0 + (unsigned long)m * a.mix_freq) % N);
-    };
-    auto adv = [&](unsigned ph, unsigned d) -> unsigned {  // (ph + d) mod N, ph,d < N
-        ph += d;
-        return ph >= N ? ph - N : ph;
-    };
-    const unsigned fstep = MIX ? (unsigned)(((unsigned long)(4 * BLOCK) % N) * a.mix_freq % N) : 0;
-    unsigned ph_t = MIX ? phase_of(b0 + 4 * (long)t) : 0;  // phase of this thread's first staged sample
-
-    if (tile == 0) {  // new history = last H samples of (history ++ mixed input)
-        uint32_t *ho = (uint32_t *)a.hist_out[ch];
-        for (int k = t; k < H; k += BLOCK) {
-            long idx = n_in - H + k;
-            uint32_t w = idx >= 0 ? in[idx] : hist[H + idx];
-            if constexpr (MIX)
-                if (idx >= 0) w = mix_sample(w, tab, N, phase_of(idx));
-            ho[k] = w;
-        }
-    }
-
-    uint4 v[PER];
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int g = t + i * BLOCK;
-        const long s = b0 + 4 * (long)g;
-        if (g < TG) {
-            if (s >= 0 && s + 3 < n_in) {
-                v[i] = *(const uint4 *)(in + s);
-                if constexpr (MIX) {
-                    unsigned ph = ph_t;
-                    v[i].x = mix_sample(v[i].x, tab, N, ph); ph = adv(ph, a.mix_freq);
-                    v[i].y = mix_sample(v[i].y, tab, N, ph); ph = adv(ph, a.mix_freq);
-                    v[i].z = mix_sample(v[i].z, tab, N, ph); ph = adv(ph, a.mix_freq);
-                    v[i].w = mix_sample(v[i].w, tab, N, ph);
-                }
-            } else {
-                uint32_t w[4];
-                unsigned ph = ph_t;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    long idx = s + j;
-                    w[j] = fetch(in, hist, idx, n_in, H);
-                    if constexpr (MIX)
-                        if (idx >= 0 && idx < n_in) w[j] = mix_sample(w[j], tab, N, ph);
-                    if constexpr (MIX) ph = adv(ph, a.mix_freq);
-                }
-                v[i] = make_uint4(w[0], w[1], w[2], w[3]);
-            }
-        }
-        if constexpr (MIX) ph_t = adv(ph_t, fstep);
-    }
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int g = t + i * BLOCK;
-        if (g < TG) {
-            int lg = PAD ? g + (g - NQ + KPAD * PR) / PR : g;
-            lds[lg] = v[i];
-        }
-    }
-    __syncthreads();
-
-    const int Bt = PAD ? NQ + KPAD + (PR + 1) * t : NQ + PR * t;
-    ConstPtr<int32_t> tp = const_view<int32_t>(a.coef);
-    int32_t Xr[4 * (NQ + R)], Xi[4 * (NQ + R)];
-    int32_t yr[R], yi[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) yr[r] = yi[r] = 0;
-    auto load_group = [&](int e) {
-        const uint4 g = lds[Bt + e + (PAD ? floordiv(e, PR) : 0)];
-        const int o = 4 * e + 4 * NQ;
-        Xr[o + 0] = sext16(g.x); Xi[o + 0] = sext16_hi(g.x);
-        Xr[o + 1] = sext16(g.y); Xi[o + 1] = sext16_hi(g.y);
-        Xr[o + 2] = sext16(g.z); Xi[o + 2] = sext16_hi(g.z);
-        Xr[o + 3] = sext16(g.w); Xi[o + 3] = sext16_hi(g.w);
-    };
-#pragma unroll
-    for (int e = -1; e < R; ++e) load_group(e);
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        if (q + 1 < NQ) load_group(-q - 2);
-        if ((q & 3) == 0) asm volatile("" : "+s"(tp));
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            const int k = 4 * q + p;
-            if (k < NT) {
-                const int32_t c = tp[k];
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const int o = 4 * (r - q) - p + 4 * NQ;
-                    yr[r] += __mul24(c, Xr[o]);  // |c| < 2^23, |x| < 2^15: v_mad_i32_i24
-                    yi[r] += __mul24(c, Xi[o]);
-                }
-            }
-        }
-    }
-    uint32_t *out = (uint32_t *)a.out + ch * a.out_stride;
-    const long n0 = o0 + (long)t * R;
-    const unsigned sh = a.shift;
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-        if (n0 + r < a.n_out) out[n0 + r] = pack16(limit16(yr[r], sh), limit16(yi[r], sh));
-}
-
 }  // namespace srcdsp
 namespace srcdsp {
 
@@ -507,7 +370,9 @@ namespace srcdsp {
 // INT_MIN there, which limitScale16 passes through and int16 truncates to 0).
 // 4 VALU ops instead of the integer path's ~8; identical results.
 __device__ __forceinline__ float q16f_shift0(float y) {
-    const float t = __builtin_fminf(__builtin_fmaxf(__builtin_truncf(y), -32767.0f), 32767.0f);
+    // "+ 0.0f" turns the -0.0 that trunc gives for y in (-1, 0) into +0.0, as the
+    // integer round trip of the reference does
+    const float t = __builtin_fminf(__builtin_fmaxf(__builtin_truncf(y), -32767.0f), 32767.0f) + 0.0f;
     return __builtin_fabsf(y) < 2147483648.0f ? t : 0.0f;
 }
 
@@ -659,6 +524,190 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
 #pragma unroll
             for (int r = 0; r < R; ++r)
                 if (n0 + r < a.n_out) out[n0 + r] = make_float2(q(yr[r]), q(yi[r]));
+        }
+    }
+}
+
+}  // namespace srcdsp
+namespace srcdsp {
+
+// Persistent complex<int16_t> x int32-tap decimator (M = 4), optionally with
+// the NCO mixer of mixers.h fused into the staging pass (config 4).
+// Same skeleton as decim_stream2_cf32: a 4-sample polyphase group is one
+// 16-B granule (4 packed words); one pad granule per lane chunk (R even) keeps
+// the lanes' ds_read_b128 conflict-free; next tile prefetched into VGPRs.
+// Products c*x with |c| < 2^23 (host-checked) are exact as v_mad_i32_i24 and
+// the int32 accumulation wraps like the reference's complex<int32_t>.
+template <int NT, int R, int BLOCK, bool MIX, int MINW>
+__global__ __launch_bounds__(BLOCK, MINW) void decim_stream_ci16(DecimLaunch a) {
+    static_assert(R % 2 == 0, "padded layout assumes an even lane chunk");
+    constexpr int NQ = (NT + 3) / 4;
+    constexpr int TO = BLOCK * R;
+    constexpr int TG = TO + NQ;  // granules of 4 samples
+    constexpr int PR = R;
+    constexpr int KPAD = ceildiv(NQ, PR);
+    constexpr int LG = TG + (TG + KPAD * PR) / PR + 1;
+    constexpr int PER = ceildiv(TG, BLOCK);
+    constexpr int TABMAX = MIX ? 4096 : 1;
+    __shared__ uint4 lds[LG];
+    __shared__ int16_t tab[TABMAX];
+
+    const int ch = blockIdx.y;
+    const uint32_t *in = (const uint32_t *)a.in + ch * a.in_stride;
+    const uint32_t *hist = (const uint32_t *)a.hist_in[ch];
+    uint32_t *out = (uint32_t *)a.out + ch * a.out_stride;
+    const long n_in = a.n_in;
+    const int H = NT - 1;
+    const int t = threadIdx.x;
+    const unsigned N = a.mix_N, fr = a.mix_freq;
+    const long nb = gridDim.x;
+    const long b = xcd_tile(blockIdx.x, nb);
+    const long per = a.ntiles / nb, rem = a.ntiles % nb;
+    const long t_begin = b * per + (b < rem ? b : rem);
+    const long t_end = t_begin + per + (b < rem ? 1 : 0);
+
+    if constexpr (MIX) {
+        for (int i = t; i < (int)N; i += BLOCK) tab[i] = a.mix_table[i];
+        __syncthreads();
+    }
+    auto adv = [&](unsigned p, unsigned d) { p += d; return p >= N ? p - N : p; };
+    // 32-bit phase arithmetic only: (base + (k mod N) * fr) mod N with k, fr < 2^16
+    auto phase_add = [&](unsigned base, unsigned k) { return (base + (k % N) * fr) % N; };
+    auto mix = [&](uint32_t w, unsigned ph) { return mix_sample(w, tab, N, ph); };
+    if (t_begin == 0 && t_end > 0) {  // new history = last H samples of (history ++ mixed input)
+        uint32_t *ho = (uint32_t *)a.hist_out[ch];
+        for (int k = t; k < H; k += BLOCK) {
+            long idx = n_in - H + k;
+            uint32_t w = idx >= 0 ? in[idx] : hist[H + idx];
+            if constexpr (MIX)  // mix_phase_hist = phase of sample n_in - H (>= 0 whenever idx >= 0)
+                if (idx >= 0) w = mix(w, idx < k ? phase_add(a.mix_phase0, (unsigned)idx)
+                                                 : phase_add(a.mix_phase_hist, (unsigned)k));
+            ho[k] = w;
+        }
+    }
+    // per-lane phase offsets of the staged granules: sample b0 + 4g, g = t + i*BLOCK
+    const unsigned d_lane = MIX ? phase_add(0, 4 * t) : 0;
+    const unsigned d_i = MIX ? phase_add(0, 4 * BLOCK) : 0;
+    // phase of a tile's first staged sample (b0 = 4*tile*TO - 4*NQ)
+    auto tile_phase = [&](long tile) {
+        return (a.mix_phase_tile0 + ((unsigned)(tile % N)) * a.mix_dtile) % N;
+    };
+
+    uint4 v[PER];
+    auto mix4 = [&](uint4 &w, unsigned ph) {
+        w.x = mix(w.x, ph); ph = adv(ph, fr);
+        w.y = mix(w.y, ph); ph = adv(ph, fr);
+        w.z = mix(w.z, ph); ph = adv(ph, fr);
+        w.w = mix(w.w, ph);
+    };
+    auto stage_load = [&](long tile) {  // tile >= 1
+        const long b0 = 4 * tile * TO - 4 * NQ;
+        const long remb = (n_in - b0) * 4;
+        const unsigned nrec = (unsigned)(remb > 0xfffffff0L ? 0xfffffff0L : (remb < 0 ? 0 : remb));
+        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)(in + b0), 0, nrec, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int g = t + i * BLOCK;
+            if (g < TG) {
+                auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * g, 0, 0);
+                v[i] = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+        }
+    };
+    // mix the staged words in registers before they go to LDS.  Past the input
+    // end the range-checked loads returned 0, and mixing 0 gives 0, so no
+    // per-lane bound checks are needed (tiles >= 1 have no negative indices).
+    auto stage_mix = [&](long tile) {
+        if constexpr (MIX) {
+            unsigned ph = adv(tile_phase(tile), d_lane);
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                if (t + i * BLOCK < TG) mix4(v[i], ph);
+                ph = adv(ph, d_i);
+            }
+        }
+    };
+    if (t_begin < t_end) {
+        if (t_begin == 0) {  // tile 0: halo from the (already mixed) history
+            const long b0 = -4 * NQ;
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int g = t + i * BLOCK;
+                const long s = b0 + 4 * (long)g;
+                if (g < TG) {
+                    uint32_t w[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        w[j] = fetch(in, hist, s + j, n_in, H);
+                        if constexpr (MIX)
+                            if (s + j >= 0 && s + j < n_in) w[j] = mix(w[j], phase_add(a.mix_phase0, (unsigned)(s + j)));
+                    }
+                    v[i] = make_uint4(w[0], w[1], w[2], w[3]);
+                }
+            }
+        } else {
+            stage_load(t_begin);
+        }
+    }
+    const int Bt = NQ + KPAD + (PR + 1) * t;
+    for (long tile = t_begin; tile < t_end; ++tile) {
+        SRCDSP_LDS_BARRIER();
+        // mixing here (after the barrier, once the prefetch has landed) keeps
+        // the compiler from hoisting it into the FMA loop (register spills)
+        if (tile != 0) stage_mix(tile);
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int g = t + i * BLOCK;
+            if (g < TG) lds[g + (g - NQ + KPAD * PR) / PR] = v[i];
+        }
+        SRCDSP_LDS_BARRIER();
+        if (tile + 1 < t_end) stage_load(tile + 1);
+
+        ConstPtr<int32_t> tp = const_view<int32_t>(a.coef);
+        asm volatile("" : "+s"(tp));
+        int32_t Xr[4 * (NQ + R)], Xi[4 * (NQ + R)];
+        int32_t yr[R], yi[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) yr[r] = yi[r] = 0;
+        auto load_group = [&](int e) {
+            const uint4 g = lds[Bt + e + floordiv(e, PR)];
+            const int o = 4 * e + 4 * NQ;
+            Xr[o + 0] = sext16(g.x); Xi[o + 0] = sext16_hi(g.x);
+            Xr[o + 1] = sext16(g.y); Xi[o + 1] = sext16_hi(g.y);
+            Xr[o + 2] = sext16(g.z); Xi[o + 2] = sext16_hi(g.z);
+            Xr[o + 3] = sext16(g.w); Xi[o + 3] = sext16_hi(g.w);
+        };
+#pragma unroll
+        for (int e = -1; e < R; ++e) load_group(e);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            if (q + 1 < NQ) load_group(-q - 2);
+            if ((q & 3) == 0) asm volatile("" : "+s"(tp));
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                const int k = 4 * q + p;
+                if (k < NT) {
+                    const int32_t c = tp[k];
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const int o = 4 * (r - q) - p + 4 * NQ;
+                        yr[r] += __mul24(c, Xr[o]);
+                        yi[r] += __mul24(c, Xi[o]);
+                    }
+                }
+            }
+        }
+        const long n0 = tile * TO + (long)t * R;
+        const unsigned sh = a.shift;
+        if (n0 + R <= a.n_out && R == 4) {
+            *(uint4 *)(out + n0) = make_uint4(pack16(limit16(yr[0], sh), limit16(yi[0], sh)),
+                                              pack16(limit16(yr[1], sh), limit16(yi[1], sh)),
+                                              pack16(limit16(yr[2], sh), limit16(yi[2], sh)),
+                                              pack16(limit16(yr[3], sh), limit16(yi[3], sh)));
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (n0 + r < a.n_out) out[n0 + r] = pack16(limit16(yr[r], sh), limit16(yi[r], sh));
         }
     }
 }

@@ -56,6 +56,10 @@ struct DecimLaunch {
     const int16_t *mix_table;
     unsigned mix_N;
     unsigned mix_phase0, mix_freq;
+    // host-precomputed phases (no 64-bit modulo on the device):
+    unsigned mix_phase_tile0;  // phase of tile 0's first staged sample (index -4*NQ)
+    unsigned mix_dtile;        // phase advance per tile (4*TO samples)
+    unsigned mix_phase_hist;   // phase of input sample n_in - H (history write-back)
     const void *hist_in[kMaxBatch];
     void *hist_out[kMaxBatch];
 };
