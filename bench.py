@@ -142,7 +142,7 @@ class CorrWorkload(Workload):
         self.x = torch.from_numpy(np.clip(x, -32768, 32767).astype(np.int16)).cuda()
         self.S = S
         self.name = "corr_1024x1"
-        self.expect = off + 1023 - 1
+        self.expect = off + 1023  # corrIndex = the peak sample (pattern end), reported one sample later
 
     def step(self):
         g = self.S.FixedPatternCorrelator(1024, 1)
@@ -176,6 +176,8 @@ def cpu_baseline(args):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     from srcdsp_amd.design import hamming_sinc
+    if args.workload in ("mixdecim", "corr"):
+        return cpu_baseline_other(args, pyoracle)
     if args.workload != "decim":
         return None
     d = os.path.join(ROOT, "oracle", "_ref", "strict")
@@ -215,6 +217,49 @@ def cpu_baseline(args):
     return {"value": round(n / secs / 1e6, 3), "unit": "Msamples/s", "cores": 1, "kind": kind,
             "sample": f"{n} samples (first {n} of channel 0 of the same synthetic workload), one step() call, "
                       f"{secs:.2f} s; {src}; host CPU: {cpu}"}
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            return next(l.split(":", 1)[1].strip() for l in fh if l.startswith("model name"))
+    except Exception:
+        return ""
+
+
+def cpu_baseline_other(args, pyoracle):
+    """Reference (oracle/_ref/strict, g++ -O2, 1 thread) for configs 4 and 5,
+    timed around the harness calls (includes its std::vector copies, a few %)."""
+    from srcdsp_amd.design import hamming_sinc, q14, qpsk_pattern
+    if not pyoracle.reference_available("strict"):
+        return None
+    ref = pyoracle.Reference("strict")
+    o = pyoracle.Oracle(0)
+    if args.workload == "mixdecim":
+        n = min(1 << 25, args.samples)
+        n -= n % 4
+        x = o.gen_ci16(SEED, 0, 0, n, -8192, 8191)
+        m = ref.mixer(4096)
+        m.reset(0.1)
+        d = ref.decim(1, 4, q14(hamming_sinc(127)))
+        t0 = time.perf_counter()
+        d.step(m.step(x))
+        secs = time.perf_counter() - t0
+        what = "Mixer<ci16,ci16,int16_t,4096>::step then FilterDnsamplingFir<ci16,ci16,ci32,int32_t,4>::step"
+    else:
+        n = min(1 << 22, args.samples)
+        p = qpsk_pattern(1024, 500, seed=2)
+        rng = np.random.default_rng(0)
+        x = np.clip(rng.integers(-125, 126, size=(n, 2)), -32768, 32767).astype(np.int16)
+        c = ref.corr(1024, 1)
+        c.set_pattern(p)
+        t0 = time.perf_counter()
+        c.step(x)
+        secs = time.perf_counter() - t0
+        what = "FixedPatternCorrelator<int16_t,int32_t,1024,1>::step (noise, no detection: full scan)"
+    return {"value": round(n / secs / 1e6, 4), "unit": "Msamples/s", "cores": 1, "kind": "reference",
+            "sample": f"{n} samples of the same workload, {secs:.2f} s; {what}; oracle/_ref/strict (g++ -O2); "
+                      f"host CPU: {_cpu_model()}"}
 
 
 def pmc_traffic(args, work_name, per_launch_samples):
@@ -284,7 +329,7 @@ def main():
             "algorithmic_bytes_per_launch": int(work.bytes_per_sample * per_launch_samples)}
     if args.workload == "corr":
         roof["bound"] = "valu"
-        roof["note"] = "integer-MAC bound (2048 MAC/sample), GB/s shown for reference only"
+        roof["note"] = "integer-MAC bound (1024 complex taps = 4096 int MAC = 2048 v_dot2 per sample), GB/s shown for reference only"
 
     if rank == 0:
         cfg = {"workload": work.name, "samples_per_channel": L, "channels_per_gpu": args.channels_per_gpu,

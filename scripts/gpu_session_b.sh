@@ -5,4 +5,4 @@ run tests_b 900 python -m pytest tests -m gpu -q --maxfail=20 ; rc=$?; [ $rc -gt
 run bench_decim 300 python bench.py || exit 1
 run bench_mixdecim 300 python bench.py --workload mixdecim --no-cpu-baseline || exit 1
 run bench_corr 600 python bench.py --workload corr --samples 67108864 --steps 3 --warmup 1 --no-cpu-baseline || exit 1
-run tune6 400 python scripts/tune/tune.py
+run prof_mix 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_mix -o run --output-format csv -- python bench.py --workload mixdecim --steps 10 --warmup 2 --no-cpu-baseline

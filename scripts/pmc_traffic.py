@@ -21,7 +21,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL_KEYS = {"decim": "decim_stream_cf32", "mixdecim": "decim_tile_ci16", "corr": "corr_eval",
+KERNEL_KEYS = {"decim": "decim_stream2_cf32", "mixdecim": "decim_stream_ci16", "corr": "corr_eval",
                "fir": "decim_generic"}
 BYTES_PER_SAMPLE = {"decim": 10.0, "mixdecim": 5.0, "corr": 4.0, "fir": 12.0}
 NAMES = {"decim": "decim_cf32_m4_t127", "mixdecim": "mixer4096_f0.1_to_decim_ci16_q14_m4_t127",

@@ -6,22 +6,22 @@
 //   out[n] = limitScale16(y[n], coeffScaling - leftShift)
 // where x[<0] is the N-1 sample history carried from the previous call.
 //
-// Kernels
-//  * decim_tile_cf32<NT,R,BLOCK,FMA>  -- the headline path: complex<float>,
-//    M = 4, NT taps.  One workgroup = one tile of BLOCK*R consecutive outputs;
-//    the tile's input span (4*BLOCK*R samples + the 4*ceil(NT/4) halo) is
-//    staged HBM -> VGPR -> LDS with 16-B coalesced loads into a padded layout
-//    (one 16-B pad per lane chunk makes the lanes' ds_read_b128 conflict-free);
-//    each lane then owns R consecutive outputs and walks the taps as 4
-//    polyphase register windows that slide by one sample per 4 taps, so every
-//    LDS read feeds 8R FMAs.  Coefficients are wave-uniform scalar loads
-//    (SGPR operands of v_fma_f32).  Each output is ONE sequential fma chain in
-//    ascending k (FMA=true), or separately rounded mul+add (FMA=false).
-//  * decim_tile_ci16<NT,R,BLOCK,MIX>  -- complex<int16_t> x int32 taps (|c|<2^23,
-//    v_mad_i32_i24), optionally with the NCO mixer of mixers.h fused into
-//    the staging pass (config 4).
-//  * decim_generic<KV,FMA>            -- any variant / M / N; one output per
-//    thread, reads through the cache.  Used for shapes without a tile kernel.
+// Kernels (decim_kernels.h)
+//  * decim_stream2_cf32<NT,R,BLOCK,FMA,MINW,Q0> -- the headline path:
+//    complex<float>, M = 4, 127/128 taps.  A persistent grid; each workgroup
+//    walks a contiguous run of tiles of BLOCK*R consecutive outputs.  A tile's
+//    input span (4*BLOCK*R samples + the 4*ceil(NT/4) halo) is staged
+//    HBM -> VGPR -> LDS (buffer_load_dwordx4, padded conflict-free layout) and
+//    the NEXT tile's loads are issued before this tile's FMA work.  Each lane
+//    owns R consecutive outputs and walks the taps as 4 polyphase register
+//    windows that slide one sample per 4 taps; taps are wave-uniform SGPR
+//    operands; each output is ONE sequential fma chain in ascending k (FMA) or
+//    separately rounded mul+add (!FMA).
+//  * decim_stream_ci16<NT,R,BLOCK,MIX,MINW> -- complex<int16_t> x int32 taps
+//    (|c| < 2^23: v_mad_i32_i24), same skeleton, optionally with the NCO mixer
+//    of mixers.h fused into the staging pass (config 4).
+//  * decim_generic<KV,FMA> -- any variant / M / N; one output per thread,
+//    reads through the cache.  Used for shapes without a tile kernel.
 // The new history (last N-1 samples of history ++ input) is written by the
 // workgroup that owns tile 0 into the other ping-pong buffer, so a step is one
 // launch.
