@@ -1,0 +1,106 @@
+// HBM streaming probes (not part of the product): what read:write mixes,
+// store/load policies and work distributions reach on MI355X, to set the
+// practical ceiling of the 4:1 decimator stream (8 B read + 2 B written per
+// input sample).
+#include <hip/hip_runtime.h>
+
+typedef float float4_t __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ float4_t ld(const float4_t *p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st(float4_t *p, float4_t v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+// RATIO input granules (16 B) per output granule; RATIO 0 = read only.
+// U output granules per lane per iteration (U*RATIO loads in flight).
+// CONTIG: block b owns a contiguous range (else grid-stride interleave).
+template <int RATIO, int U, bool NTL, bool NTS, bool CONTIG>
+__global__ __launch_bounds__(256) void rw_probe(const float4_t *in, float4_t *out, long n_out) {
+    const long nth = (long)gridDim.x * 256;
+    const int t = threadIdx.x;
+    long begin, end, step, lane0;
+    if constexpr (CONTIG) {
+        const long per = (n_out + gridDim.x - 1) / gridDim.x;
+        begin = blockIdx.x * per;
+        end = begin + per < n_out ? begin + per : n_out;
+        step = 256L * U;
+        lane0 = t;
+    } else {
+        begin = 0;
+        end = n_out;
+        step = nth * U;
+        lane0 = (long)blockIdx.x * 256 + t;
+    }
+    const long sub = CONTIG ? 256 : nth;  // distance between a lane's U outputs
+    float4_t acc = {0, 0, 0, 0};
+    for (long base = begin; base + step <= end; base += step) {
+        float4_t v[U * (RATIO > 0 ? RATIO : 4)];
+        constexpr int R = RATIO > 0 ? RATIO : 4;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long o = base + lane0 + u * sub;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                // a wave reads R contiguous KiB runs: granule (o - lane) * R + r * 64... keep coalesced:
+                // input granule index = R*(o - lane0_wave) + r*64 + lane_in_wave
+                const long ow = o - (t & 63);
+                v[u * R + r] = ld<NTL>(in + R * ow + r * 64 + (t & 63));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            float4_t s = v[u * R];
+#pragma unroll
+            for (int r = 1; r < R; ++r) s += v[u * R + r];
+            if constexpr (RATIO > 0) st<NTS>(out + base + lane0 + u * sub, s);
+            else acc += s;
+        }
+    }
+    if constexpr (RATIO == 0)
+        if (acc.x == 1234.5f) out[0] = acc;
+}
+
+__global__ __launch_bounds__(256) void fill_probe(float4_t *out, long n) {
+    const long nth = (long)gridDim.x * 256;
+    const float4_t z = {1, 2, 3, 4};
+    for (long k = (long)blockIdx.x * 256 + threadIdx.x; k < n; k += nth) out[k] = z;
+}
+
+#define CASE(id, R, U, NL, NS, C)                                                                  \
+    case id:                                                                                       \
+        hipLaunchKernelGGL((rw_probe<R, U, NL, NS, C>), dim3(blocks), dim3(256), 0, s, in, out,    \
+                           (R) > 0 ? n_in16 / (R) : n_in16 / 4);                                    \
+        break;
+
+extern "C" int bw_probe(int id, int blocks, const void *in_, void *out_, long n_in16, void *stream) {
+    const float4_t *in = (const float4_t *)in_;
+    float4_t *out = (float4_t *)out_;
+    hipStream_t s = (hipStream_t)stream;
+    switch (id) {
+        CASE(0, 1, 2, false, false, false)  // copy 1:1
+        CASE(1, 4, 1, false, false, false)  // 4:1 grid-stride, 4 loads in flight
+        CASE(2, 4, 2, false, false, false)  // 4:1, 8 loads in flight
+        CASE(3, 4, 2, false, true, false)   // 4:1 nt stores
+        CASE(4, 4, 2, true, false, false)   // 4:1 nt loads
+        CASE(5, 4, 2, true, true, false)    // 4:1 nt both
+        CASE(6, 4, 1, false, false, true)   // 4:1 contiguous per block
+        CASE(7, 4, 2, false, false, true)   // 4:1 contiguous, 8 in flight
+        CASE(8, 4, 2, false, true, true)    // 4:1 contiguous, nt stores
+        CASE(9, 0, 2, false, false, false)  // read only
+        CASE(10, 0, 2, true, false, false)  // read only nt
+        CASE(11, 4, 4, false, false, false) // 4:1, 16 loads in flight
+        CASE(12, 1, 2, false, true, false)  // copy nt stores
+    case 20:
+        hipLaunchKernelGGL(fill_probe, dim3(blocks), dim3(256), 0, s, out, n_in16 / 4);
+        break;
+    default:
+        return -1;
+    }
+    return hipGetLastError();
+}
