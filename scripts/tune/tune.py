@@ -59,21 +59,25 @@ def main():
     cdev = torch.from_numpy(c).cuda()
     S.FilterDnsamplingFir(c, 4).step(x, ref)
     lib.tune_stream_probe.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_long, C.c_void_p]
-    for blocks in (1024, 2048, 4096, 8192):
+    for blocks in (() if not os.environ.get("TUNE_PROBES") else (1024, 2048, 4096, 8192)):
         fn = lambda: lib.tune_stream_probe(blocks, C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), L, stream)
         fn()
         med, mn = timeit(fn, 10)
         print(f"  streaming ceiling probe (8 B in / 2 B out per sample), {blocks} blocks: {mn:.4f} ms "
               f"-> {10 * L / (mn * 1e-3) / 1e9:.1f} GB/s")
     lib.tune_stream_probe2.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_long, C.c_void_p]
-    for mode, label, bps in ((0, "coalesced 4:1 stream (10 B/sample)", 10), (1, "read-only stream (8 B/sample)", 8)):
+    for mode, label, bps in (((0, "coalesced 4:1 stream (10 B/sample)", 10), (1, "read-only stream (8 B/sample)", 8))
+                             if os.environ.get("TUNE_PROBES") else ()):
         for blocks in (2048, 4096, 8192, 16384):
             fn = lambda: lib.tune_stream_probe2(mode, blocks, C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), L,
                                                 stream)
             fn()
             med, mn = timeit(fn, 10)
             print(f"  {label}, {blocks} blocks: {mn:.4f} ms -> {bps * L / (mn * 1e-3) / 1e9:.1f} GB/s")
-    variants = [(11, 2048, "v2 R4 B256 g2048"), (30, 2048, "v2 +nt loads"), (20, 2048, "PROBE mem-only R4 B256")]
+    variants = [(11, 2048, "v2 R4 B256 g2048"), (30, 2048, "v2 +nt loads"), (40, 2048, "v2 GS g2048"),
+                (40, 1024, "v2 GS g1024"), (41, 2048, "v2 GS +ntl g2048"), (41, 1024, "v2 GS +ntl g1024"),
+                (42, 1024, "v2 GS +ntl +staged nts g1024"), (43, 1024, "PROBE mem-only GS g1024"),
+                (43, 2048, "PROBE mem-only GS g2048")]
     res = {v: [] for v in variants}
     for rnd in range(int(os.environ.get('TUNE_ROUNDS', '6'))):
         for v in variants:

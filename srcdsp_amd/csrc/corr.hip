@@ -100,7 +100,8 @@ __global__ __launch_bounds__(kCorrBlock) void corr_eval(const uint32_t *__restri
                                                         long i_end, const uint32_t *__restrict__ hist,
                                                         const int32_t *__restrict__ coef, unsigned N, unsigned S,
                                                         unsigned cs, uint32_t *__restrict__ corr_out,
-                                                        uint32_t *__restrict__ en_out) {
+                                                        uint32_t *__restrict__ en_out, const unsigned *stop) {
+    if ((long)*stop < i_begin) return;  // an earlier segment already detected
     extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
     const long NSm1 = (long)N * S - 1;
     const long span = kCorrBlock + NSm1;  // samples i0-NSm1 .. i0+255
@@ -153,7 +154,8 @@ __global__ __launch_bounds__(kCBlock) void corr_eval_s1(const uint32_t *__restri
                                                          long i_end, const uint32_t *__restrict__ hist,
                                                          const uint32_t *__restrict__ ptaps, int N, unsigned cs,
                                                          uint32_t *__restrict__ corr_out,
-                                                         uint32_t *__restrict__ en_out) {
+                                                         uint32_t *__restrict__ en_out, const unsigned *stop) {
+    if ((long)*stop < i_begin) return;  // an earlier segment already detected
     extern __shared__ __attribute__((aligned(16))) uint32_t xs[];
     constexpr int TO = kCBlock * kCR;
     const long i0 = i_begin + (long)blockIdx.x * TO;  // first output of the tile
@@ -241,6 +243,9 @@ __global__ __launch_bounds__(kCBlock) void corr_eval_s1(const uint32_t *__restri
 
 __global__ void corr_detect(const uint32_t *__restrict__ corr, const uint32_t *__restrict__ en, long i_begin,
                             long i_end, uint32_t c_prev0, uint32_t c_prev1, uint32_t e_prev0, unsigned *best) {
+    // skip when an EARLIER segment detected (a hit of this segment is >= i_begin,
+    // so blocks of this launch never stop each other)
+    if ((long)*(volatile unsigned *)best < i_begin) return;
     for (long i = i_begin + (long)blockIdx.x * blockDim.x + threadIdx.x; i < i_end;
          i += (long)gridDim.x * blockDim.x) {
         const uint32_t c0 = corr[i];
@@ -287,34 +292,36 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
     const uint32_t *hist = c.d_hist[c.cur];
     const unsigned cs = (unsigned)c.coeff_scaling;
     const bool fast = c.S == 1 && c.N % 16 == 0 && c.taps16;
-    // The reference stops at the first detection (break, correlators.h:291):
-    // scan in segments and stop after the first segment holding one.
-    const long seg = std::max<long>(1L << 23, (n + 7) / 8);
+    // The reference stops at the first detection (break, correlators.h:291).
+    // All segments are queued at once; each launch returns at its start when
+    // an earlier segment's detect kernel has recorded a hit, so the scan stops
+    // one segment after the detection with no host round trip in between.
+    const long seg = std::max<long>(1L << 22, (n + 15) / 16);
     const unsigned none = 0xffffffffu;
     unsigned best = none;
-    for (long sb = 0; sb < n && best == none; sb += seg) {
+    SRCDSP_HIP_TRY(hipMemsetAsync(c.d_best, 0xff, 4, s));
+    for (long sb = 0; sb < n; sb += seg) {
         const long se = std::min(n, sb + seg);
         if (fast) {
             constexpr long TO = (long)kCBlock * kCR;
             const long blocks = (se - sb + TO - 1) / TO;
             const size_t smem = 4 * (size_t)(((TO + c.N + 1) / kCR + 2) * (kCR + 4));
             hipLaunchKernelGGL(corr_eval_s1, dim3((unsigned)blocks), dim3(kCBlock), smem, s, d_in, n, sb, se, hist,
-                               c.d_ptaps, (int)c.N, cs, c.d_corr, c.d_en);
+                               c.d_ptaps, (int)c.N, cs, c.d_corr, c.d_en, (const unsigned *)c.d_best);
         } else {
             const size_t smem = 4 * (size_t)((kCorrBlock + NSm1 + 3) & ~3l) + 8 * (size_t)c.N;
             const long blocks = (se - sb + kCorrBlock - 1) / kCorrBlock;
             hipLaunchKernelGGL(corr_eval, dim3((unsigned)blocks), dim3(kCorrBlock), smem, s, d_in, n, sb, se, hist,
-                               c.d_coef, c.N, c.S, cs, c.d_corr, c.d_en);
+                               c.d_coef, c.N, c.S, cs, c.d_corr, c.d_en, (const unsigned *)c.d_best);
         }
         SRCDSP_HIP_TRY(hipGetLastError());
-        SRCDSP_HIP_TRY(hipMemcpyAsync(c.d_best, &none, 4, hipMemcpyHostToDevice, s));
         const int db = (int)std::max<long>(1, std::min<long>((se - sb + 255) / 256, 4096));
         hipLaunchKernelGGL(corr_detect, dim3(db), dim3(256), 0, s, c.d_corr, c.d_en, sb, se, c.corr[0], c.corr[1],
                            c.energy[0], c.d_best);
         SRCDSP_HIP_TRY(hipGetLastError());
-        SRCDSP_HIP_TRY(hipMemcpyAsync(&best, c.d_best, 4, hipMemcpyDeviceToHost, s));
-        SRCDSP_HIP_TRY(hipStreamSynchronize(s));
     }
+    SRCDSP_HIP_TRY(hipMemcpyAsync(&best, c.d_best, 4, hipMemcpyDeviceToHost, s));
+    SRCDSP_HIP_TRY(hipStreamSynchronize(s));
 
     const bool hit = best != none;
     const long last = hit ? (long)best : n - 1;  // last processed sample

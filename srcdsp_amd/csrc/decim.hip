@@ -26,6 +26,7 @@
 // workgroup that owns tile 0 into the other ping-pong buffer, so a step is one
 // launch.
 #include <algorithm>
+#include <vector>
 
 #include "ops.h"
 
@@ -78,6 +79,18 @@ int launch_ci16(DecimLaunch L, int channels, bool mixed, hipStream_t s) {
     return SRCDSP_OK;
 }
 
+template <int NT>
+int launch_ci16_dot2(DecimLaunch L, int channels, bool mixed, hipStream_t s) {
+    constexpr int TO = kCiBlock * kCiR;  // = 4 * 256: phase_step_tile assumes this tile
+    L.ntiles = (L.n_out + TO - 1) / TO;
+    dim3 grid((unsigned)std::min<long>(L.ntiles, kCfGridCap), channels);
+    if (mixed)
+        hipLaunchKernelGGL((decim_dot2_ci16<NT, kCiBlock, true, 4>), grid, dim3(kCiBlock), 0, s, L);
+    else
+        hipLaunchKernelGGL((decim_dot2_ci16<NT, kCiBlock, false, 4>), grid, dim3(kCiBlock), 0, s, L);
+    return SRCDSP_OK;
+}
+
 template <int KV>
 int launch_generic(const DecimLaunch &L, int channels, unsigned M, bool fma, hipStream_t s) {
     long blocks = std::max<long>(1, std::min<long>((L.n_out + 255) / 256, 4096));
@@ -99,6 +112,10 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
     int rc = SRCDSP_OK;
     if (f.M == 4 && f.kv == KV_CF32 && al && (f.ntaps == 127 || f.ntaps == 128)) {
         rc = f.ntaps == 127 ? launch_cf32<127>(L, channels, fma, s) : launch_cf32<128>(L, channels, fma, s);
+    } else if (f.M == 4 && f.kv == KV_CI16_I32 && f.coef_fits_i16 && al && (f.ntaps == 127 || f.ntaps == 128)) {
+        DecimLaunch L2 = L;
+        L2.coef = f.d_cpair;
+        rc = f.ntaps == 127 ? launch_ci16_dot2<127>(L2, channels, mixed, s) : launch_ci16_dot2<128>(L2, channels, mixed, s);
     } else if (f.M == 4 && f.kv == KV_CI16_I32 && f.coef_fits_i24 && al && (f.ntaps == 127 || f.ntaps == 128)) {
         rc = f.ntaps == 127 ? launch_ci16<127>(L, channels, mixed, s) : launch_ci16<128>(L, channels, mixed, s);
     } else {
@@ -121,6 +138,12 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
 }
 
 // ================================================================ FirCore
+static bool coef_i16(const int32_t *c, int n) {
+    for (int i = 0; i < n; ++i)
+        if (c[i] > 32767 || c[i] < -32768) return false;
+    return true;
+}
+
 static bool coef_i24(const int32_t *c, int n) {
     for (int i = 0; i < n; ++i)
         if (c[i] >= (1 << 23) || c[i] < -(1 << 23)) return false;
@@ -146,8 +169,20 @@ int FirCore::set_coeffs(const void *coeffs, int n, bool keep_history) {
             coeff_scaling = coeff_scaling_i32((const int32_t *)coeffs, n);
     }
     coef_fits_i24 = (kv == KV_CI16_I32) && coef_i24((const int32_t *)tmp.data(), n);
+    coef_fits_i16 = (kv == KV_CI16_I32) && coef_i16((const int32_t *)tmp.data(), n);
     if (d_coef) (void)hipFree(d_coef);
     d_coef = nullptr;
+    if (d_cpair) (void)hipFree(d_cpair);
+    d_cpair = nullptr;
+    if (coef_fits_i16) {  // tap pairs for v_dot2: P_j = (lo c[2j], hi c[2j-1]), c[-1] = c[n] = 0
+        const int32_t *c = (const int32_t *)tmp.data();
+        auto tap = [&](int k) { return (k >= 0 && k < n) ? (uint32_t)(uint16_t)(int16_t)c[k] : 0u; };
+        const int J = n / 2 + 1;
+        std::vector<uint32_t> pr((size_t)J);
+        for (int j = 0; j < J; ++j) pr[j] = tap(2 * j) | (tap(2 * j - 1) << 16);
+        SRCDSP_HIP_TRY(hipMalloc(&d_cpair, 4 * (size_t)J));
+        SRCDSP_HIP_TRY(hipMemcpy(d_cpair, pr.data(), 4 * (size_t)J, hipMemcpyHostToDevice));
+    }
     SRCDSP_HIP_TRY(hipMalloc(&d_coef, 4 * (size_t)n));
     SRCDSP_HIP_TRY(hipMemcpy(d_coef, tmp.data(), 4 * (size_t)n, hipMemcpyHostToDevice));
 
@@ -196,6 +231,8 @@ int FirCore::clear_history() {
 void FirCore::destroy() {
     (void)order.sync();
     if (d_coef) (void)hipFree(d_coef);
+    if (d_cpair) (void)hipFree(d_cpair);
+    d_cpair = nullptr;
     for (int b = 0; b < 2; ++b)
         if (d_hist[b]) (void)hipFree(d_hist[b]);
     d_coef = nullptr;

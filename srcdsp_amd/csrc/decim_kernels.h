@@ -5,6 +5,7 @@
 #include "ops.h"
 
 namespace srcdsp {
+typedef short short2_t_ __attribute__((ext_vector_type(2)));
 
 // Taps of the tile kernels are read through a CONSTANT-address-space view of
 // the device coefficient buffer: wave-uniform s_load into SGPRs, consumed as
@@ -384,8 +385,20 @@ __device__ __forceinline__ float q16f_shift0(float y) {
 // PROBE (tuning only): 0 = real kernel; 1 = memory path only (no FMA loop);
 // 2 = compute path only (every tile reads the same L2-resident input span)
 // NTL: non-temporal (streaming) input loads; OST: outputs staged through LDS
-// so each store instruction writes whole contiguous lines.
-template <int NT, int R, int BLOCK, bool FMA, int MINW, bool Q0, int PROBE = 0, bool NTL = false, bool OST = false>
+// so each store instruction writes whole contiguous lines; NTS: non-temporal
+// output stores.
+template <bool NTS>
+__device__ __forceinline__ void store16(float4 *p, float4 v) {
+    if constexpr (NTS) {
+        typedef float f4_t __attribute__((ext_vector_type(4)));
+        f4_t w = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(w, (f4_t *)p);
+    } else {
+        *p = v;
+    }
+}
+template <int NT, int R, int BLOCK, bool FMA, int MINW, bool Q0, int PROBE = 0, bool NTL = false, bool OST = false,
+          bool NTS = false, bool GS = false>
 __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a) {
     constexpr int NQ = (NT + 3) / 4;
     constexpr int TO = BLOCK * R;
@@ -406,8 +419,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
     const long nb = gridDim.x;
     const long b = xcd_tile(blockIdx.x, nb);
     const long per = a.ntiles / nb, rem = a.ntiles % nb;
-    const long t_begin = b * per + (b < rem ? b : rem);
-    const long t_end = t_begin + per + (b < rem ? 1 : 0);
+    // GS: tiles b, b+nb, b+2nb, ... (the whole grid sweeps one contiguous
+    // window of the input at a time); else a contiguous run of tiles per block
+    const long t_begin = GS ? b : b * per + (b < rem ? b : rem);
+    const long t_end = GS ? a.ntiles : t_begin + per + (b < rem ? 1 : 0);
+    constexpr long kStep1 = 1;
+    const long t_step = GS ? nb : kStep1;
     if (t_begin == 0 && t_end > 0) write_history(in, n_in, hist, (float2 *)a.hist_out[ch], H);
 
     float4 v[PER];
@@ -445,7 +462,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
         }
     }
     const int Bt = 2 * NQ + KPAD + (PR + 1) * t;
-    for (long tile = t_begin; tile < t_end; ++tile) {
+    for (long tile = t_begin; tile < t_end; tile += t_step) {
         SRCDSP_LDS_BARRIER();
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
@@ -453,7 +470,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
             if (g < TG) lds[g + (g - 2 * NQ + KPAD * PR) / PR] = v[i];
         }
         SRCDSP_LDS_BARRIER();
-        if (tile + 1 < t_end) stage_load(tile + 1);
+        if (tile + t_step < t_end) stage_load(tile + t_step);
 
         ConstPtr<float> tp = const_view<float>(a.coef);
         asm volatile("" : "+s"(tp));
@@ -510,7 +527,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
 #pragma unroll
                 for (int i = 0; i < TO / 2 / BLOCK; ++i) {
                     const int k = t + i * BLOCK;
-                    *(float4 *)(out + o0 + 2 * k) = ob4[k];
+                    store16<NTS>((float4 *)(out + o0 + 2 * k), ob4[k]);
                 }
             } else {
                 for (int k = t; k < TO; k += BLOCK)
@@ -519,7 +536,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
         } else if (n0 + R <= a.n_out && (R % 2) == 0) {
 #pragma unroll
             for (int r = 0; r < R; r += 2)
-                *(float4 *)(out + n0 + r) = make_float4(q(yr[r]), q(yi[r]), q(yr[r + 1]), q(yi[r + 1]));
+                store16<NTS>((float4 *)(out + n0 + r), make_float4(q(yr[r]), q(yi[r]), q(yr[r + 1]), q(yi[r + 1])));
         } else {
 #pragma unroll
             for (int r = 0; r < R; ++r)
@@ -700,6 +717,230 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream_ci16(DecimLaunch a) 
         const long n0 = tile * TO + (long)t * R;
         const unsigned sh = a.shift;
         if (n0 + R <= a.n_out && R == 4) {
+            *(uint4 *)(out + n0) = make_uint4(pack16(limit16(yr[0], sh), limit16(yi[0], sh)),
+                                              pack16(limit16(yr[1], sh), limit16(yi[1], sh)),
+                                              pack16(limit16(yr[2], sh), limit16(yi[2], sh)),
+                                              pack16(limit16(yr[3], sh), limit16(yi[3], sh)));
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (n0 + r < a.n_out) out[n0 + r] = pack16(limit16(yr[r], sh), limit16(yi[r], sh));
+        }
+    }
+}
+
+// ------------------------------------------------- ci16 x int16-range taps
+// Persistent complex<int16_t> decimator (M = 4) on v_dot2_i32_i16: each dot2
+// is TWO taps of one component.  The staged samples are split into a real
+// and an imaginary plane of packed int16 pairs (x[2e], x[2e+1]); with the taps
+// paired as P_j = (lo c[2j], hi c[2j-1]) (c[-1] = c[NT] = 0) output r of a
+// lane (input sample 4r of its chunk) is
+//   y_r = sum_{j=0}^{J-1} dot2(D[2r - j], P_j),  D[d] = plane dword d,
+// so a lane's 4 outputs slide ONE register window down the plane by one dword
+// per tap pair: 8 dot2 per pair, one ds_read_b128 per plane every 4 pairs.
+// Products int16 x int16 and the int32 accumulation wrap exactly as the
+// reference's complex<int32_t> arithmetic (host checks |c| <= 32767).
+// Fused mixer (MIX): the LDS table holds (lo T[(k+N/4)%N], hi T[k]) = (lr, li);
+// re = dot2(x, (lr, -li)), im = dot2(swap(x), (lr, li)).
+// LDS: per plane granule G (8 samples), slot 5*(G>>1) + (G&1) + 2*plane, slot
+// 4 of each 5 is padding: the lanes of a ds_read_b128 group (granules 2t+c)
+// land on 16 distinct 16-B bank slots.
+__device__ __forceinline__ int32_t clamp_s14(int32_t v) {
+    const int32_t a = v >> 14;  // |v| < 2^30: never INT_MIN
+    return a > 32767 ? 32767 : (a < -32767 ? -32767 : a);
+}
+__device__ __forceinline__ uint32_t lo16_pair(uint32_t a, uint32_t b) {  // (lo a, lo b)
+    return __builtin_amdgcn_perm(b, a, 0x05040100u);
+}
+__device__ __forceinline__ uint32_t hi16_pair(uint32_t a, uint32_t b) {  // (hi a, hi b)
+    return __builtin_amdgcn_perm(b, a, 0x07060302u);
+}
+__device__ __forceinline__ int32_t sdot2(uint32_t a, uint32_t b, int32_t c) {
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t_, a), __builtin_bit_cast(short2_t_, b), c, false);
+}
+// mixers.h:169-188 on one packed sample with the (lr, li) table word
+__device__ __forceinline__ void mix_dot2(uint32_t w, uint32_t C, int32_t &re, int32_t &im) {
+    const uint32_t A = __builtin_bit_cast(uint32_t, __builtin_bit_cast(short2_t_, C) * (short2_t_){1, -1});
+    const uint32_t ws = __builtin_amdgcn_alignbit(w, w, 16);
+    re = clamp_s14(sdot2(w, A, 0));
+    im = clamp_s14(sdot2(ws, C, 0));
+}
+
+template <int NT, int BLOCK, bool MIX, int MINW>
+__global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
+    constexpr int R = 4;
+    constexpr int J = NT / 2 + 1;                 // tap pairs
+    constexpr int HS = 16 * ceildiv(2 * (J - 1), 16);  // halo samples (lane-chunk aligned)
+    constexpr int HG = HS / 8;                    // halo plane granules
+    constexpr int TO = BLOCK * R;                 // outputs per tile
+    constexpr int TG = (4 * TO + HS) / 4;         // staged 16-B sample granules
+    constexpr int PER = ceildiv(TG, BLOCK);
+    constexpr int PG = (4 * TO + HS) / 8;         // plane granules
+    constexpr int LSLOTS = 5 * ceildiv(PG, 2);
+    constexpr int TABMAX = MIX ? 4096 : 1;
+    static_assert(HS % 16 == 0 && 2 * (J - 1) <= HS, "halo geometry");
+    __shared__ uint4 lds[LSLOTS];
+    __shared__ uint32_t ctab[TABMAX];
+
+    const int ch = blockIdx.y;
+    const uint32_t *in = (const uint32_t *)a.in + ch * a.in_stride;
+    const uint32_t *hist = (const uint32_t *)a.hist_in[ch];
+    uint32_t *out = (uint32_t *)a.out + ch * a.out_stride;
+    const long n_in = a.n_in;
+    const int H = NT - 1;
+    const int t = threadIdx.x;
+    const unsigned N = a.mix_N, fr = a.mix_freq;
+    const long nb = gridDim.x;
+    const long b = xcd_tile(blockIdx.x, nb);
+    const long per = a.ntiles / nb, rem = a.ntiles % nb;
+    const long t_begin = b * per + (b < rem ? b : rem);
+    const long t_end = t_begin + per + (b < rem ? 1 : 0);
+
+    if constexpr (MIX) {
+        const int16_t *tab = a.mix_table;
+        for (int i = t; i < (int)N; i += BLOCK) {
+            unsigned ic = i + N / 4;
+            ic = ic >= N ? ic - N : ic;
+            ctab[i] = ((uint32_t)(uint16_t)tab[ic]) | ((uint32_t)(uint16_t)tab[i] << 16);
+        }
+        __syncthreads();
+    }
+    auto adv = [&](unsigned p, unsigned d) { p += d; const unsigned q = p - N; return q < p ? q : p; };
+    auto phase_add = [&](unsigned base, unsigned k) { return (base + (k % N) * fr) % N; };
+    auto mix1 = [&](uint32_t w, unsigned ph) {
+        int32_t re, im;
+        mix_dot2(w, ctab[ph], re, im);
+        return pack16(re, im);
+    };
+    if (t_begin == 0 && t_end > 0) {  // new history = last H samples of (history ++ mixed input)
+        uint32_t *ho = (uint32_t *)a.hist_out[ch];
+        for (int k = t; k < H; k += BLOCK) {
+            long idx = n_in - H + k;
+            uint32_t w = idx >= 0 ? in[idx] : hist[H + idx];
+            if constexpr (MIX)
+                if (idx >= 0) w = mix1(w, idx < k ? phase_add(a.mix_phase0, (unsigned)idx)
+                                                  : phase_add(a.mix_phase_hist, (unsigned)k));
+            ho[k] = w;
+        }
+    }
+    const unsigned d_lane = MIX ? phase_add(0, 4 * t) : 0;
+    const unsigned d_i = MIX ? phase_add(0, 4 * BLOCK) : 0;
+    auto tile_phase = [&](long tile) {  // phase of the tile's first staged sample 4*tile*TO - HS
+        return (a.mix_phase_tile0 + ((unsigned)(tile % N)) * a.mix_dtile) % N;
+    };
+
+    uint4 v[PER];
+    auto stage_load = [&](long tile) {  // tile >= 1
+        const long b0 = 4 * tile * TO - HS;
+        const long remb = (n_in - b0) * 4;
+        const unsigned nrec = (unsigned)(remb > 0xfffffff0L ? 0xfffffff0L : (remb < 0 ? 0 : remb));
+        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)(in + b0), 0, nrec, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int g = t + i * BLOCK;
+            if (g < TG) {
+                auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * g, 0, 0);
+                v[i] = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+        }
+    };
+    // staged granule g -> plane granule g>>1, half g&1
+    auto lds_half = [&](int g, int plane) {
+        const int G = g >> 1;
+        return (uint2 *)&lds[5 * (G >> 1) + (G & 1) + 2 * plane] + (g & 1);
+    };
+    auto put = [&](int g, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+        *lds_half(g, 0) = make_uint2(lo16_pair(w0, w1), lo16_pair(w2, w3));
+        *lds_half(g, 1) = make_uint2(hi16_pair(w0, w1), hi16_pair(w2, w3));
+    };
+    // mixes the granule in place (MIX) and writes both planes
+    auto put_mixed = [&](int g, uint4 w, unsigned ph) {
+        if constexpr (MIX) {
+            int32_t r0, i0, r1, i1, r2, i2, r3, i3;
+            mix_dot2(w.x, ctab[ph], r0, i0); ph = adv(ph, fr);
+            mix_dot2(w.y, ctab[ph], r1, i1); ph = adv(ph, fr);
+            mix_dot2(w.z, ctab[ph], r2, i2); ph = adv(ph, fr);
+            mix_dot2(w.w, ctab[ph], r3, i3);
+            *lds_half(g, 0) = make_uint2(lo16_pair(r0, r1), lo16_pair(r2, r3));
+            *lds_half(g, 1) = make_uint2(lo16_pair(i0, i1), lo16_pair(i2, i3));
+        } else {
+            put(g, w.x, w.y, w.z, w.w);
+        }
+    };
+    if (t_begin < t_end) {
+        if (t_begin == 0) {  // tile 0: halo from the (already mixed) history; mixed here, written below
+            const long b0 = -HS;
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int g = t + i * BLOCK;
+                const long s0 = b0 + 4 * (long)g;
+                if (g < TG) {
+                    uint32_t w[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        w[j] = fetch(in, hist, s0 + j, n_in, H);
+                        if constexpr (MIX)
+                            if (s0 + j >= 0 && s0 + j < n_in) w[j] = mix1(w[j], phase_add(a.mix_phase0, (unsigned)(s0 + j)));
+                    }
+                    v[i] = make_uint4(w[0], w[1], w[2], w[3]);
+                }
+            }
+        } else {
+            stage_load(t_begin);
+        }
+    }
+    const int lb = 2 * t + HG;  // lane's first plane granule
+    for (long tile = t_begin; tile < t_end; ++tile) {
+        SRCDSP_LDS_BARRIER();
+        if (MIX && tile != 0) {
+            unsigned ph = adv(tile_phase(tile), d_lane);
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int g = t + i * BLOCK;
+                if (g < TG) put_mixed(g, v[i], ph);
+                ph = adv(ph, d_i);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int g = t + i * BLOCK;
+                if (g < TG) put(g, v[i].x, v[i].y, v[i].z, v[i].w);
+            }
+        }
+        SRCDSP_LDS_BARRIER();
+        if (tile + 1 < t_end) stage_load(tile + 1);
+
+        ConstPtr<uint32_t> tp = const_view<uint32_t>(a.coef);
+        asm volatile("" : "+s"(tp));
+        // window: Dr[d + OFF], d in [-(4*NG), 8), NG = granules below the lane base
+        constexpr int NG = ceildiv(J - 1, 4);
+        constexpr int OFF = 4 * NG;
+        uint32_t Dr[OFF + 8], Di[OFF + 8];
+        auto load_g = [&](int c) {  // plane granule lb + c -> dwords d = 4c .. 4c+3
+            const uint4 gr = lds[5 * ((lb + c) >> 1) + ((lb + c) & 1)];
+            const uint4 gi = lds[5 * ((lb + c) >> 1) + ((lb + c) & 1) + 2];
+            Dr[OFF + 4 * c + 0] = gr.x; Dr[OFF + 4 * c + 1] = gr.y; Dr[OFF + 4 * c + 2] = gr.z; Dr[OFF + 4 * c + 3] = gr.w;
+            Di[OFF + 4 * c + 0] = gi.x; Di[OFF + 4 * c + 1] = gi.y; Di[OFF + 4 * c + 2] = gi.z; Di[OFF + 4 * c + 3] = gi.w;
+        };
+        load_g(0);
+        load_g(1);
+        int32_t yr[R], yi[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) yr[r] = yi[r] = 0;
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            if ((j & 3) == 1) load_g(-1 - (j >> 2));
+            if ((j & 15) == 0) asm volatile("" : "+s"(tp));
+            const uint32_t P = tp[j];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                yr[r] = sdot2(Dr[OFF + 2 * r - j], P, yr[r]);
+                yi[r] = sdot2(Di[OFF + 2 * r - j], P, yi[r]);
+            }
+        }
+        const long n0 = tile * TO + (long)t * R;
+        const unsigned sh = a.shift;
+        if (n0 + R <= a.n_out) {
             *(uint4 *)(out + n0) = make_uint4(pack16(limit16(yr[0], sh), limit16(yi[0], sh)),
                                               pack16(limit16(yr[1], sh), limit16(yi[1], sh)),
                                               pack16(limit16(yr[2], sh), limit16(yi[2], sh)),

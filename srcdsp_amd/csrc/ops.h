@@ -24,7 +24,9 @@ struct FirCore {
     unsigned coeff_scaling = 0;  // as the reference stores it (unsigned)
     int left_shift = 0;
     bool coef_fits_i24 = false;   // integer taps usable by v_mad_i32_i24
+    bool coef_fits_i16 = false;   // int32 taps all in int16 range: v_dot2 tap pairs
     void *d_coef = nullptr;       // float[N] or int32[N] (int16 taps widened)
+    uint32_t *d_cpair = nullptr;  // N/2+1 packed tap pairs (lo c[2j], hi c[2j-1]) when coef_fits_i16
     std::string h_coef;           // host copy of the taps as given (batch compatibility)
     void *d_hist[2] = {nullptr, nullptr};
     size_t hist_cap = 0;          // bytes per history buffer

@@ -118,6 +118,45 @@ def test_decim_ci16_tile_and_mixer_chain_vs_oracle(S, O):
         assert m.state()[:2] == om.state()[:2]
 
 
+@pytest.mark.parametrize("ntaps", [127, 128])
+@pytest.mark.parametrize("kind", ["i16", "i24", "i32"])
+def test_decim_ci16_tap_ranges_vs_oracle(S, O, ntaps, kind):
+    """int16-range taps run the v_dot2 kernel, |c| < 2^23 the v_mad_i32_i24
+    kernel, anything wider the generic one; all bit-exact, including int32
+    accumulator wrap-around and saturation on full-scale inputs."""
+    rng = np.random.default_rng(ntaps + len(kind))
+    lim = {"i16": 32767, "i24": (1 << 23) - 1, "i32": (1 << 24)}[kind]
+    c = rng.integers(-lim, lim + 1, size=ntaps).astype(np.int32)
+    c[0], c[-1], c[ntaps // 2] = lim, -lim - 1 if kind == "i16" else -lim, 1
+    x = O["strict"].gen_ci16(99, 2, 0, (1 << 18) + 4096, -32768, 32767)
+    g = S.FilterDnsamplingFir(c, 4, "complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int32_t")
+    r = O["strict"].decim(1, 4, c)
+    for off, n in _chunks(len(x), [65536, 4, 8196, 100000]):
+        n -= n % 4
+        xs = x[off:off + n]
+        assert np.array_equal(g.step(dev(xs)).cpu().numpy(), r.step(xs)), (off, n)
+
+
+@pytest.mark.parametrize("N,f", [(1000, -0.37), (4096, 0.73), (2048, 0.0)])
+def test_mixdecim_chain_table_sizes(S, O, N, f):
+    """Fused mixer (LDS (cos, sin) table, dot2 complex multiply) at
+    non-power-of-two and power-of-two table sizes, several chained calls."""
+    from srcdsp_amd.design import hamming_sinc, q14
+    cq = q14(hamming_sinc(127))
+    x = O["strict"].gen_ci16(0xBEE, 3, 0, 400000, -32768, 32767)
+    m = S.Mixer(N)
+    m.reset(f)
+    d = S.FilterDnsamplingFir(cq, 4, "complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int32_t")
+    chain = S.MixerDecimatorChain(m, d)
+    om, od = O["strict"].mixer(N), O["strict"].decim(1, 4, cq)
+    om.reset(f)
+    for off, n in _chunks(len(x), [131072, 8, 4100, 200000]):
+        n -= n % 4
+        xs = x[off:off + n]
+        assert np.array_equal(chain.step(dev(xs)).cpu().numpy(), od.step(om.step(xs))), (off, n)
+        assert m.state()[:2] == om.state()[:2]
+
+
 def test_decim_batched_equals_single(S, O):
     import torch
     from srcdsp_amd.design import hamming_sinc
