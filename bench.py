@@ -42,7 +42,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", default="decim", choices=["decim", "mixdecim", "corr", "fir"])
+    p.add_argument("--workload", default="decim", choices=["decim", "mixdecim", "corr", "fir", "up"])
     p.add_argument("--samples", type=int, default=1 << 28, help="input samples per channel per step")
     p.add_argument("--channels-per-gpu", type=int, default=1)
     p.add_argument("--fp", default="fma", choices=["fma", "strict"])
@@ -130,21 +130,30 @@ class MixDecimWorkload(Workload):
 
 
 class CorrWorkload(Workload):
+    """Config 5.  One 64 Msamp buffer; at N > 1 it is split in time (SURVEY
+    8e): rank r primes its correlator with the N*S+2 samples before its share,
+    scans its share, and the first detection is a MIN all-reduce over RCCL."""
     dtype = "i32"
     bytes_per_sample = 4.0
 
     def __init__(self, S, torch, L, channels, rank, fp):
+        from srcdsp_amd import dist as D
         from srcdsp_amd.design import qpsk_pattern
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.p = qpsk_pattern(1024, 500, seed=2)
-        rng = np.random.default_rng(rank)
+        rng = np.random.default_rng(0)  # the same global buffer on every rank
         x = rng.integers(-125, 126, size=(L, 2)).astype(np.int32)
         off = (3 * L) // 4
         x[off:off + 1024] += 2 * self.p
-        self.x = torch.from_numpy(np.clip(x, -32768, 32767).astype(np.int16)).cuda()
-        self.S = S
+        x = np.clip(x, -32768, 32767).astype(np.int16)
+        self.s0, s1 = D.time_segment(L, self.world, rank)
+        hc = min(self.s0, D.corr_halo(1024, 1))
+        self.halo = torch.from_numpy(x[self.s0 - hc:self.s0]).cuda() if hc else None
+        self.x = torch.from_numpy(x[self.s0:s1]).cuda()
+        del x
+        self.S, self.D = S, D
         self.name = "corr_1024x1"
         self.expect = off + 1023  # corrIndex = the peak sample (pattern end), reported one sample later
-
         self.g = S.FixedPatternCorrelator(1024, 1)
         self.g.setPattern(self.p)
 
@@ -152,8 +161,10 @@ class CorrWorkload(Workload):
         # one independent 64 Msamp buffer per step: reset() (correlators.h:196)
         # clears the registers and history, then one step() scans to the hit
         self.g.reset()
-        found, idx = self.g.step(self.x)
-        self.last = (found, idx)
+        local = self.D.corr_segment_search(self.g, self.halo, self.x, self.s0)
+        first = self.D.first_detection(local, self.world, device="cuda")
+        found = first != self.D.NO_DETECTION
+        self.last = (found, first if found else -1)
 
 
 class FirWorkload(Workload):
@@ -171,7 +182,28 @@ class FirWorkload(Workload):
         self.f.step(self.x, self.y)
 
 
-WORKLOADS = {"decim": DecimWorkload, "mixdecim": MixDecimWorkload, "corr": CorrWorkload, "fir": FirWorkload}
+class UpWorkload(Workload):
+    """FilterUpsamplingFir<ci16,ci16,ci32,int32_t,4> (a7; not a BASELINE config):
+    128-tap Q14 interpolator, L = 4, input length L samples -> 4L outputs."""
+    dtype = "i32"
+    bytes_per_sample = 20.0  # 4 B complex<int16_t> in, 4 x 4 B out per input sample
+
+    def __init__(self, S, torch, L, channels, rank, fp):
+        from srcdsp_amd.design import hamming_sinc, q14
+        n = L // 4  # keep the output (4n samples) the size of the other workloads' input
+        self.x = torch.empty((n, 2), dtype=torch.int16, device="cuda")
+        S.fill_synthetic(self.x, "ci16", seed=SEED, channel=rank, lo=-8192, hi=8191)
+        self.y = torch.empty((4 * n, 2), dtype=torch.int16, device="cuda")
+        self.f = S.FilterUpsamplingFir(q14(hamming_sinc(128, 0.12) * 4), 4)
+        self.n = n
+        self.name = "up_ci16_q14_l4_t128"
+
+    def step(self):
+        self.f.step(self.x, self.y)
+
+
+WORKLOADS = {"decim": DecimWorkload, "mixdecim": MixDecimWorkload, "corr": CorrWorkload, "fir": FirWorkload,
+             "up": UpWorkload}
 
 
 # ---------------------------------------------------------------- CPU baseline
@@ -312,6 +344,8 @@ def main():
     kern_avg_ms = float(np.mean(kern_ms))
 
     units_per_rank = L * (args.channels_per_gpu if args.workload == "decim" else 1) * args.steps
+    if args.workload == "up":
+        units_per_rank = work.n * args.steps
     total_samples = units_per_rank * world
     value = total_samples / wall / 1e6
     ms_per_step = wall / args.steps * 1e3
@@ -327,6 +361,8 @@ def main():
         del bufs
 
     per_launch_samples = L * args.channels_per_gpu if args.workload == "decim" else L
+    if args.workload == "up":
+        per_launch_samples = work.n
     achieved = work.bytes_per_sample * per_launch_samples / (kern_avg_ms * 1e-3) / 1e9
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args, work.name, per_launch_samples),
@@ -337,8 +373,8 @@ def main():
         # 2048 v_dot2 lane-ops per scanned sample; the reference scans up to and
         # including the detected sample.  Peak: 256 CUs x 64 lanes x 2.4 GHz.
         found, idx = work.last
-        scanned = (idx + 2) if found else L
-        dot2_tops = 2048.0 * scanned / (kern_avg_ms * 1e-3) / 1e12
+        scanned = (idx + 2) if found else L  # single-buffer reference scan length
+        dot2_tops = 2048.0 * scanned / world / (kern_avg_ms * 1e-3) / 1e12  # per GPU
         roof = {"bound": "valu", "achieved": round(dot2_tops, 2), "peak": VALU_PEAK_TOPS,
                 "unit": "T v_dot2 lane-ops/s", "frac": round(dot2_tops / VALU_PEAK_TOPS, 4), "traffic": None,
                 "kernel": work.name, "kernel_ms": round(kern_avg_ms, 4), "scanned_samples": int(scanned),
@@ -346,13 +382,17 @@ def main():
 
     if rank == 0:
         cfg = {"workload": work.name, "samples_per_channel": L, "channels_per_gpu": args.channels_per_gpu,
-               "taps": 127 if args.workload in ("decim", "mixdecim") else None, "decimation": 4,
-               "fp_contract": args.fp, "parallelism": f"channels sharded over {world} GPU(s)",
+               "taps": {"decim": 127, "mixdecim": 127, "fir": 31, "up": 128}.get(args.workload),
+               "decimation": {"decim": 4, "mixdecim": 4}.get(args.workload), "interpolation": 4 if args.workload == "up" else None,
+               "fp_contract": args.fp,
+               "parallelism": (f"one buffer split in time over {world} GPU(s), first detection by MIN all-reduce"
+                               if args.workload == "corr" else f"channels sharded over {world} GPU(s)"),
                "timed": "device-resident input, one step() per step; PCIe excluded"}
         line = {"metric": METRIC if args.workload == "decim" else f"Msamples/sec (in), {work.name}",
                 "value": round(value, 2), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-                "scaling": "weak", "vs_baseline": None, "dtype": work.dtype,
+                "scaling": "strong" if args.workload == "corr" and world > 1 else "weak",
+                "vs_baseline": None, "dtype": work.dtype,
                 "data": "synthetic (counter-based splitmix64 integer samples, SURVEY §8d)", "config": cfg,
                 "roofline": roof}
         if gather_ms is not None:

@@ -159,6 +159,11 @@ SRCDSP_API int srcdsp_mixer_adjust_frequency(srcdsp_mixer_t h, float adjust);
 /* phase, frequency word, nominal frequency; and the N-entry LUT (host copy) */
 SRCDSP_API int srcdsp_mixer_get_state(srcdsp_mixer_t h, int *phi, int *freq, float *nominal);
 SRCDSP_API int srcdsp_mixer_get_table(srcdsp_mixer_t h, int16_t *table_host);
+/* Extension (no reference call; SURVEY 8e time sharding): set the phase
+ * accumulator phi (0 <= phi < N), the closed form (phi0 + k*freq) mod N of
+ * mixers.h:177 at sample k, so a buffer segment starting at sample k mixes
+ * exactly as the unsplit buffer. */
+SRCDSP_API int srcdsp_mixer_set_phase(srcdsp_mixer_t h, int phi);
 /* step  mixers.h:169-188 ; n_out == n_in */
 SRCDSP_API int srcdsp_mixer_step(srcdsp_mixer_t h, const void *d_in, size_t n, void *d_out, void *stream);
 SRCDSP_API int srcdsp_mixer_step_host(srcdsp_mixer_t h, const void *in, size_t n, void *out);
@@ -189,6 +194,11 @@ SRCDSP_API int srcdsp_corr_step(srcdsp_corr_t h, const void *d_in, size_t n, int
                                 void *stream);
 SRCDSP_API int srcdsp_corr_step_host(srcdsp_corr_t h, const void *in, size_t n, int *found,
                                      int *corr_index);
+/* Extension (no reference call; SURVEY 8e time sharding): the state step()
+ * leaves after streaming these n samples with NO detection test
+ * (correlators.h:221-250 without :262-291): history ring and the
+ * energy/correlation registers.  Seeds a time segment with its halo. */
+SRCDSP_API int srcdsp_corr_prime(srcdsp_corr_t h, const void *d_in, size_t n, void *stream);
 /* getRefBitSamples  correlators.h:311-316 (N complex<int16_t>, host copy) */
 SRCDSP_API int srcdsp_corr_get_bit_samples(srcdsp_corr_t h, int16_t *bits_host);
 /* getStatus  correlators.h:90 (CorrState fields) */

@@ -123,6 +123,7 @@ class Oracle:
             "corr_pattern": _sig(lib, "orc_corr_set_pattern", None, VP, VP, D),
             "corr_reset": _sig(lib, "orc_corr_reset", None, VP),
             "corr_step": _sig(lib, "orc_corr_step", I, VP, VP, L, VP),
+            "corr_prime": _sig(lib, "orc_corr_prime", None, VP, VP, L),
             "corr_bits": _sig(lib, "orc_corr_bit_samples", None, VP, VP),
             "corr_status": _sig(lib, "orc_corr_status", None, VP, VP, VP, VP, VP, VP),
             "corr_destroy": _sig(lib, "orc_corr_destroy", None, VP),
@@ -278,6 +279,11 @@ class _Corr(_Handle):
         idx = C.c_int(-12345)
         found = self.o.f["corr_step"](self._h, _ptr(x), len(x), C.byref(idx))
         return bool(found), idx.value
+
+    def prime(self, x):
+        """State after streaming x with no detection (not a reference call)."""
+        x = as_kind(x, "ci16")
+        self.o.f["corr_prime"](self._h, _ptr(x), len(x))
 
     def bit_samples(self):
         b = np.zeros((self.N, 2), np.int16)

@@ -549,7 +549,8 @@ void orc_corr_reset(orc_corr *c) {  /* :146-159 */
 }
 
 /* step (correlators.h:209-303) */
-int orc_corr_step(orc_corr *c, const int16_t *in, long n, int *corr_index) {
+/* detect = 0: stream the samples without the detection test (orc_corr_prime) */
+static int corr_run(orc_corr *c, const int16_t *in, long n, int *corr_index, int detect) {
     const long H = (long)c->H, S = (long)c->S, N = (long)c->N;
     for (long idx = 0; idx < n; ++idx) {
         long top = (long)c->top;
@@ -582,7 +583,7 @@ int orc_corr_step(orc_corr *c, const int16_t *in, long n, int *corr_index) {
         c->corr[1] = c->corr[0];
         int32_t ar = tr >> 2, ai = ti >> 2;
         c->corr[0] = (uint32_t)wadd(wmul(ar, ar), wmul(ai, ai));   /* :250 */
-        if (c->corr[1] > c->corr[2] && c->corr[1] > c->corr[0]) {  /* :262 */
+        if (detect && c->corr[1] > c->corr[2] && c->corr[1] > c->corr[0]) {  /* :262 */
             double cm = sqrt((double)c->corr[1]);
             double em = sqrt((double)c->energy[1]);
             if (cm > em * 2.7 && em > 300) {                        /* :265-268 */
@@ -602,6 +603,18 @@ int orc_corr_step(orc_corr *c, const int16_t *in, long n, int *corr_index) {
         c->top = (size_t)((top + 1) % H);
     }
     return 0;
+}
+
+int orc_corr_step(orc_corr *c, const int16_t *in, long n, int *corr_index) {
+    return corr_run(c, in, n, corr_index, 1);
+}
+
+/* Not a reference call: the state the correlator has after streaming `in`
+ * with no detection in it (used to seed a time segment with its halo, so a
+ * buffer split over ranks finds the same first detection). */
+void orc_corr_prime(orc_corr *c, const int16_t *in, long n) {
+    int dummy = 0;
+    (void)corr_run(c, in, n, &dummy, 0);
 }
 
 void orc_corr_bit_samples(const orc_corr *c, int16_t *out) { memcpy(out, c->bits, 4 * (size_t)c->N); }

@@ -74,10 +74,12 @@ def main():
             fn()
             med, mn = timeit(fn, 10)
             print(f"  {label}, {blocks} blocks: {mn:.4f} ms -> {bps * L / (mn * 1e-3) / 1e9:.1f} GB/s")
-    variants = [(11, 2048, "v2 R4 B256 g2048"), (30, 2048, "v2 +nt loads"), (40, 2048, "v2 GS g2048"),
-                (40, 1024, "v2 GS g1024"), (41, 2048, "v2 GS +ntl g2048"), (41, 1024, "v2 GS +ntl g1024"),
-                (42, 1024, "v2 GS +ntl +staged nts g1024"), (43, 1024, "PROBE mem-only GS g1024"),
-                (43, 2048, "PROBE mem-only GS g2048")]
+    variants = [(11, 2048, "v2 R4 B256 g2048"), (40, 2048, "v2 GS g2048"), (41, 2048, "v2 GS +ntl g2048"),
+                (42, 1024, "v2 GS +ntl +staged nts g1024"), (42, 2048, "v2 GS +ntl +staged nts g2048"),
+                (44, 2048, "v2 GS +staged nts g2048"), (36, 2048, "v2 +staged nts g2048")]
+    if os.environ.get("TUNE_SUSTAINED_ONLY"):
+        sustained_rounds(variants, x, y, cdev, h0, h1, stream, L, ref)
+        return
     res = {v: [] for v in variants}
     for rnd in range(int(os.environ.get('TUNE_ROUNDS', '6'))):
         for v in variants:
@@ -100,6 +102,35 @@ def main():
         print(f"  {v[2]:28s} {res[v][0]:8s} {tmin:.4f} ms  {L / tmin / 1e6:8.1f} Gsamp/s  {gbs:7.1f} GB/s "
               f"({gbs / 8000 * 100:.1f}% of 8 TB/s)")
     sustained(variants, x, y, cdev, h0, h1, stream, L)
+
+
+def sustained_rounds(variants, x, y, cdev, h0, h1, stream, L, ref, rounds=4, reps=30):
+    """Interleaved rounds of back-to-back launches (the bench's pattern): per
+    round and variant the median of the last 20 launches; min/median over rounds."""
+    res = {v: [] for v in variants}
+    for v in variants:  # correctness first
+        y.zero_()
+        lib.tune_decim(v[0], v[1], C.c_void_p(cdev.data_ptr()), C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()),
+                       L, C.c_void_p(h0.data_ptr()), C.c_void_p(h1.data_ptr()), stream)
+        torch.cuda.synchronize()
+        assert torch.equal(y.view(torch.int32), ref.view(torch.int32)), v
+    st = torch.cuda.current_stream()
+    for rnd in range(rounds):
+        for v in variants:
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+            for i in range(reps):
+                ev[i][0].record(st)
+                lib.tune_decim(v[0], v[1], C.c_void_p(cdev.data_ptr()), C.c_void_p(x.data_ptr()),
+                               C.c_void_p(y.data_ptr()), L, C.c_void_p(h0.data_ptr()), C.c_void_p(h1.data_ptr()),
+                               stream)
+                ev[i][1].record(st)
+            torch.cuda.synchronize()
+            res[v].append(float(np.median([a.elapsed_time(b) for a, b in ev][-20:])))
+    print(f"sustained, {rounds} interleaved rounds x {reps} launches (median of last 20 per round):", flush=True)
+    for v in variants:
+        r = res[v]
+        print(f"  {v[2]:32s} min {min(r):.4f}  median {np.median(r):.4f} ms -> {10 * L / (np.median(r) * 1e-3) / 1e9:7.1f} GB/s"
+              f"  rounds {' '.join(f'{t:.4f}' for t in r)}", flush=True)
 
 
 def sustained(variants, x, y, cdev, h0, h1, stream, L, reps=60):

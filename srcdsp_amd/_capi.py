@@ -52,6 +52,7 @@ SIGNATURES = {
     "srcdsp_mixer_reset": (I, [VP, F]),
     "srcdsp_mixer_adjust_frequency": (I, [VP, F]),
     "srcdsp_mixer_get_state": (I, [VP, IP, IP, FP]),
+    "srcdsp_mixer_set_phase": (I, [VP, I]),
     "srcdsp_mixer_get_table": (I, [VP, I16P]),
     "srcdsp_mixer_step": (I, [VP, VP, SZ, VP, VP]),
     "srcdsp_mixer_step_host": (I, [VP, VP, SZ, VP]),
@@ -61,6 +62,7 @@ SIGNATURES = {
     "srcdsp_corr_set_pattern": (I, [VP, I32P, D]),
     "srcdsp_corr_reset": (I, [VP]),
     "srcdsp_corr_step": (I, [VP, VP, SZ, IP, IP, VP]),
+    "srcdsp_corr_prime": (I, [VP, VP, SZ, VP]),
     "srcdsp_corr_step_host": (I, [VP, VP, SZ, IP, IP]),
     "srcdsp_corr_get_bit_samples": (I, [VP, I16P]),
     "srcdsp_corr_get_status": (I, [VP, U32P, U32P, U32P, IP, DP]),

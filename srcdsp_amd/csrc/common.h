@@ -75,6 +75,20 @@ __device__ __forceinline__ long xcd_tile(long bid, long nb) {
     return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
 }
 
+// Taps of the tile kernels are read through a CONSTANT-address-space view of
+// the device coefficient buffer: wave-uniform s_load into SGPRs, consumed as
+// the scalar operand of each FMA.  (Through a plain pointer the compiler must
+// assume the taps may alias the outputs and uses vector loads into VGPRs.)
+// The view is made opaque every 16 taps so the scalar loads are not all
+// hoisted to the top of the tile (127 live SGPRs would spill).
+template <typename T>
+using ConstPtr = const __attribute__((address_space(4))) T *;
+
+template <typename T>
+__device__ __forceinline__ ConstPtr<T> const_view(const void *p) {
+    return (ConstPtr<T>)p;
+}
+
 constexpr int floordiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
 constexpr int ceildiv(int a, int b) { return (a + b - 1) / b; }
 

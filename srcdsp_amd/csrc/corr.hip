@@ -275,8 +275,10 @@ static int corr_alloc_scratch(srcdsp_corr_state &c, size_t n) {
     return SRCDSP_OK;
 }
 
+// detect = false: stream the samples with no detection test (corr_prime):
+// only the last three positions are evaluated (they feed the registers).
 static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *found, int *corr_index,
-                    hipStream_t s) {
+                    hipStream_t s, bool detect = true) {
     *found = 0;
     if (n_ == 0) return SRCDSP_OK;
     const long n = (long)n_;
@@ -300,7 +302,7 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
     const unsigned none = 0xffffffffu;
     unsigned best = none;
     SRCDSP_HIP_TRY(hipMemsetAsync(c.d_best, 0xff, 4, s));
-    for (long sb = 0; sb < n; sb += seg) {
+    for (long sb = detect ? 0 : std::max(0L, n - 3); sb < n; sb += seg) {
         const long se = std::min(n, sb + seg);
         if (fast) {
             constexpr long TO = (long)kCBlock * kCR;
@@ -315,6 +317,7 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
                                c.d_coef, c.N, c.S, cs, c.d_corr, c.d_en, (const unsigned *)c.d_best);
         }
         SRCDSP_HIP_TRY(hipGetLastError());
+        if (!detect) continue;
         const int db = (int)std::max<long>(1, std::min<long>((se - sb + 255) / 256, 4096));
         hipLaunchKernelGGL(corr_detect, dim3(db), dim3(256), 0, s, c.d_corr, c.d_en, sb, se, c.corr[0], c.corr[1],
                            c.energy[0], c.d_best);
@@ -483,6 +486,12 @@ SRCDSP_API int srcdsp_corr_reset(srcdsp_corr_t h) {
     SRCDSP_HIP_TRY(hipMemset(c.d_hist[c.cur], 0, hb));
     SRCDSP_HIP_TRY(hipDeviceSynchronize());
     return SRCDSP_OK;
+}
+
+SRCDSP_API int srcdsp_corr_prime(srcdsp_corr_t h, const void *d_in, size_t n, void *stream) {
+    SRCDSP_ARG_CHECK(h != nullptr && (d_in != nullptr || n == 0), "corr_prime: null argument");
+    int found = 0, idx = 0;
+    return corr_run(h->c, (const uint32_t *)d_in, n, &found, &idx, (hipStream_t)stream, false);
 }
 
 SRCDSP_API int srcdsp_corr_step(srcdsp_corr_t h, const void *d_in, size_t n, int *found, int *corr_index,

@@ -56,14 +56,21 @@ int launch_cf32(DecimLaunch L, int channels, bool fma, hipStream_t s) {
     L.ntiles = (L.n_out + TO - 1) / TO;
     dim3 grid((unsigned)std::min<long>(L.ntiles, kCfGridCap), channels);
     const bool q0 = (L.shift & 31u) == 0;  // limitScale16 shift 0: the 4-op float quantiser
+    // measured best (scripts/tune, sustained back-to-back): grid-stride tile
+    // order (GS), non-temporal input loads, outputs staged through LDS into
+    // whole-line non-temporal stores -- 5.7 % over contiguous runs / plain ops
     if (fma && q0)
-        hipLaunchKernelGGL((decim_stream2_cf32<NT, kCfR, kCfBlock, true, 4, true>), grid, dim3(kCfBlock), 0, s, L);
+        hipLaunchKernelGGL((decim_stream2_cf32<NT, kCfR, kCfBlock, true, 4, true, 0, true, true, true, true>), grid,
+                           dim3(kCfBlock), 0, s, L);
     else if (fma)
-        hipLaunchKernelGGL((decim_stream2_cf32<NT, kCfR, kCfBlock, true, 4, false>), grid, dim3(kCfBlock), 0, s, L);
+        hipLaunchKernelGGL((decim_stream2_cf32<NT, kCfR, kCfBlock, true, 4, false, 0, true, true, true, true>), grid,
+                           dim3(kCfBlock), 0, s, L);
     else if (q0)
-        hipLaunchKernelGGL((decim_stream2_cf32<NT, kCfR, kCfBlock, false, 3, true>), grid, dim3(kCfBlock), 0, s, L);
+        hipLaunchKernelGGL((decim_stream2_cf32<NT, kCfR, kCfBlock, false, 3, true, 0, true, true, true, true>), grid,
+                           dim3(kCfBlock), 0, s, L);
     else
-        hipLaunchKernelGGL((decim_stream2_cf32<NT, kCfR, kCfBlock, false, 3, false>), grid, dim3(kCfBlock), 0, s, L);
+        hipLaunchKernelGGL((decim_stream2_cf32<NT, kCfR, kCfBlock, false, 3, false, 0, true, true, true, true>), grid,
+                           dim3(kCfBlock), 0, s, L);
     return SRCDSP_OK;
 }
 
@@ -92,6 +99,22 @@ int launch_ci16_dot2(DecimLaunch L, int channels, bool mixed, hipStream_t s) {
 }
 
 template <int KV>
+int launch_fir_tile(const DecimLaunch &L, int channels, bool fma, hipStream_t s) {
+    constexpr int TO = kFirR * kFirBlock;
+    constexpr int SPG = FirTraits<KV>::SPG;
+    const int NQ = (L.ntaps + 3) / 4;
+    const int P0 = 8 * ((NQ + 1) / 2);
+    const int span = TO + P0;
+    const size_t smem = 16 * (size_t)(span / SPG + span / SPG / (kFirR / SPG) + 1);
+    dim3 grid((unsigned)((L.n_out + TO - 1) / TO), channels);
+    if (fma)
+        hipLaunchKernelGGL((fir_tile_f32<KV, true>), grid, dim3(kFirBlock), smem, s, L);
+    else
+        hipLaunchKernelGGL((fir_tile_f32<KV, false>), grid, dim3(kFirBlock), smem, s, L);
+    return SRCDSP_OK;
+}
+
+template <int KV>
 int launch_generic(const DecimLaunch &L, int channels, unsigned M, bool fma, hipStream_t s) {
     long blocks = std::max<long>(1, std::min<long>((L.n_out + 255) / 256, 4096));
     dim3 grid((unsigned)blocks, channels);
@@ -110,7 +133,11 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
     const bool fma = !(f.flags & SRCDSP_FLAG_FP_STRICT);
     bool al = aligned16(L.in) && ((L.in_stride * kv_in_bytes(f.kv)) % 16 == 0);
     int rc = SRCDSP_OK;
-    if (f.M == 4 && f.kv == KV_CF32 && al && (f.ntaps == 127 || f.ntaps == 128)) {
+    const bool out_al = aligned16(L.out) && ((L.out_stride * kv_out_bytes(f.kv)) % 16 == 0);
+    if (f.M == 1 && (f.kv == KV_CF32 || f.kv == KV_F32_REAL) && al && out_al && f.ntaps <= kFirMaxTaps && !mixed) {
+        rc = f.kv == KV_CF32 ? launch_fir_tile<KV_CF32>(L, channels, fma, s)
+                             : launch_fir_tile<KV_F32_REAL>(L, channels, fma, s);
+    } else if (f.M == 4 && f.kv == KV_CF32 && al && (f.ntaps == 127 || f.ntaps == 128)) {
         rc = f.ntaps == 127 ? launch_cf32<127>(L, channels, fma, s) : launch_cf32<128>(L, channels, fma, s);
     } else if (f.M == 4 && f.kv == KV_CI16_I32 && f.coef_fits_i16 && al && (f.ntaps == 127 || f.ntaps == 128)) {
         DecimLaunch L2 = L;

@@ -7,20 +7,6 @@
 namespace srcdsp {
 typedef short short2_t_ __attribute__((ext_vector_type(2)));
 
-// Taps of the tile kernels are read through a CONSTANT-address-space view of
-// the device coefficient buffer: wave-uniform s_load into SGPRs, consumed as
-// the scalar operand of each FMA.  (Through a plain pointer the compiler must
-// assume the taps may alias the outputs and uses vector loads into VGPRs.)
-// The view is made opaque every 16 taps so the scalar loads are not all
-// hoisted to the top of the tile (127 live SGPRs would spill).
-template <typename T>
-using ConstPtr = const __attribute__((address_space(4))) T *;
-
-template <typename T>
-__device__ __forceinline__ ConstPtr<T> const_view(const void *p) {
-    return (ConstPtr<T>)p;
-}
-
 // ------------------------------------------------------------ arithmetic
 template <bool FMA>
 __device__ __forceinline__ float mac(float c, float x, float y) {
@@ -950,6 +936,154 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
             for (int r = 0; r < R; ++r)
                 if (n0 + r < a.n_out) out[n0 + r] = pack16(limit16(yr[r], sh), limit16(yi[r], sh));
         }
+    }
+}
+
+// ------------------------------------------------------ single-rate float FIR
+// FilterFir (filters.h:133-169) and M = 1 decimators for complex<float> input
+// (KV_CF32) and float input -> complex<float> output with a zero imaginary
+// part (KV_F32_REAL), any tap count up to kFirMaxTaps (runtime).
+// Each lane owns R = 8 consecutive outputs; taps are walked in chunks of 4
+// with a 12-sample register window held as three 4-sample blocks A|B|C (tap
+// chunk q of output r reads sample r - 4q - p, p < 4).  After a chunk C drops,
+// B -> C, A -> B and A is refilled from LDS, so three chunks are unrolled with
+// rotating block roles and the window slides without register moves.  Each
+// output is ONE sequential fma (or mul+add) chain in ascending tap order, as
+// the reference's loop over n (filters.h:150-161).
+// LDS: the tile span (tile outputs + P0 halo samples, P0 = 8*ceil((N-1)/8))
+// as 16-B granules with one pad granule after every lane chunk (8 samples),
+// so lanes' ds_read_b128 land on distinct bank slots (odd granule stride).
+constexpr int kFirMaxTaps = 1024;
+typedef float f2_t __attribute__((ext_vector_type(2)));
+constexpr int kFirR = 8, kFirBlock = 256;
+
+template <int KV>
+struct FirTraits;
+template <>
+struct FirTraits<KV_F32_REAL> {
+    typedef float S;
+    static constexpr int SPG = 4;  // samples per 16-B granule
+};
+template <>
+struct FirTraits<KV_CF32> {
+    typedef float2 S;
+    static constexpr int SPG = 2;
+};
+
+__device__ __forceinline__ float fir_mac(bool fma, float c, float x, float y) {
+    return fma ? __builtin_fmaf(c, x, y) : y + c * x;
+}
+
+template <int KV, bool FMA>
+__global__ __launch_bounds__(kFirBlock) void fir_tile_f32(DecimLaunch a) {
+    typedef typename FirTraits<KV>::S S;
+    constexpr int SPG = FirTraits<KV>::SPG;
+    constexpr int R = kFirR, BLOCK = kFirBlock, TO = R * BLOCK;
+    constexpr int GPL = R / SPG;  // granules per lane chunk
+    extern __shared__ float4 fl[];
+    const int N = a.ntaps, H = N - 1;
+    const int NQ = (N + 3) / 4;
+    const int P0 = 8 * ((NQ + 1) / 2);  // >= 4*NQ: the last chunk's window block
+    const int ch = blockIdx.y;
+    const S *in = (const S *)a.in + ch * a.in_stride;
+    const S *hist = (const S *)a.hist_in[ch];
+    float2 *out = (float2 *)a.out + ch * a.out_stride;
+    const long n_in = a.n_in;
+    const int t = threadIdx.x;
+    if (blockIdx.x == 0) write_history(in, n_in, hist, (S *)a.hist_out[ch], H);
+    const long o0 = (long)blockIdx.x * TO;  // first output (= input sample) of the tile
+    const int span = TO + P0;                // staged samples, origin o0 - P0
+    auto slot = [&](int g) { return g + g / GPL; };
+    // stage: granule-wise, through the cache (halo from history on tile 0)
+    for (int g = t; g < span / SPG; g += BLOCK) {
+        const long s0 = o0 - P0 + (long)g * SPG;
+        float4 v;
+        if (s0 >= 0 && s0 + SPG <= n_in) {
+            v = *(const float4 *)(in + s0);
+        } else {
+            S w[SPG];
+#pragma unroll
+            for (int j = 0; j < SPG; ++j) w[j] = fetch(in, hist, s0 + j, n_in, H);
+            v = *(const float4 *)w;
+        }
+        fl[slot(g)] = v;
+    }
+    __syncthreads();
+    // lane base sample b = P0 + R*t; window sample m (relative to b) lives in
+    // granule (b + m) / SPG at slot(...)
+    const int gb = (P0 + R * t) / SPG;
+    float yr[R];
+    f2_t y2[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        yr[r] = 0.f;
+        y2[r] = (f2_t){0.f, 0.f};
+    }
+    S A[4], B[4], C[4];
+    auto fill = [&](S (&dst)[4], int m) {
+        if constexpr (SPG == 4) {
+            const float4 v = fl[slot(gb + m / 4)];
+            dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
+        } else {
+            const float4 v0 = fl[slot(gb + m / 2)], v1 = fl[slot(gb + m / 2 + 1)];
+            dst[0] = make_float2(v0.x, v0.y); dst[1] = make_float2(v0.z, v0.w);
+            dst[2] = make_float2(v1.x, v1.y); dst[3] = make_float2(v1.z, v1.w);
+        }
+    };
+    ConstPtr<float> tp = const_view<float>(a.coef);
+    // chunk q: window blocks (lo = samples -4q-4.., mid = -4q.., hi = -4q+4..)
+    auto chunk = [&](int q, const S (&lo)[4], const S (&mid)[4], const S (&hi)[4], bool guard) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int k = 4 * q + p;
+            if (guard && k >= N) break;
+            const float c = tp[k];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int rel = r - p + 4;  // 0..11 over lo|mid|hi
+                const S x = rel < 4 ? lo[rel] : (rel < 8 ? mid[rel - 4] : hi[rel - 8]);
+                if constexpr (SPG == 4) {
+                    yr[r] = fir_mac(FMA, c, x, yr[r]);
+                } else {  // (re, im) as one packed pair: v_pk_fma_f32 / v_pk_mul + v_pk_add
+                    const f2_t xv = {x.x, x.y}, cv = {c, c};
+                    if constexpr (FMA) y2[r] = __builtin_elementwise_fma(cv, xv, y2[r]);
+                    else y2[r] = y2[r] + cv * xv;
+                }
+            }
+        }
+    };
+    fill(C, 4);
+    fill(B, 0);
+    int q = 0;
+    for (; q + 3 <= NQ; q += 3) {
+        asm volatile("" : "+s"(tp));
+        fill(A, -4 * q - 4);
+        chunk(q, A, B, C, false);          // A|B|C
+        fill(C, -4 * q - 8);
+        chunk(q + 1, C, A, B, false);      // C|A|B
+        fill(B, -4 * q - 12);
+        chunk(q + 2, B, C, A, q + 3 == NQ);  // B|C|A (guard the last chunk)
+    }
+    if (q < NQ) {
+        fill(A, -4 * q - 4);
+        chunk(q, A, B, C, true);
+        if (q + 1 < NQ) {
+            fill(C, -4 * q - 8);
+            chunk(q + 1, C, A, B, true);
+        }
+    }
+    const unsigned sh = a.shift;
+    const long n0 = o0 + (long)t * R;
+    float2 o[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        o[r] = SPG == 4 ? make_float2(q16f(yr[r], sh), 0.f) : make_float2(q16f(y2[r].x, sh), q16f(y2[r].y, sh));
+    if (n0 + R <= a.n_out) {
+#pragma unroll
+        for (int r = 0; r < R; r += 2) *(float4 *)(out + n0 + r) = make_float4(o[r].x, o[r].y, o[r + 1].x, o[r + 1].y);
+    } else {
+        for (int r = 0; r < R; ++r)
+            if (n0 + r < a.n_out) out[n0 + r] = o[r];
     }
 }
 

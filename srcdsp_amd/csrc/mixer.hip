@@ -191,6 +191,15 @@ SRCDSP_API int srcdsp_mixer_adjust_frequency(srcdsp_mixer_t h, float adj) {
     return SRCDSP_OK;
 }
 
+SRCDSP_API int srcdsp_mixer_set_phase(srcdsp_mixer_t h, int phi) {
+    SRCDSP_ARG_CHECK(h != nullptr, "mixer_set_phase: null handle");
+    SRCDSP_ARG_CHECK(phi >= 0 && (unsigned)phi < h->m.N, "mixer_set_phase: phi must be in [0, N)");
+    int rc = h->m.order.sync();
+    if (rc) return rc;
+    h->m.phi = (int16_t)phi;
+    return SRCDSP_OK;
+}
+
 SRCDSP_API int srcdsp_mixer_get_state(srcdsp_mixer_t h, int *phi, int *freq, float *nominal) {
     SRCDSP_ARG_CHECK(h != nullptr, "mixer_get_state: null handle");
     if (phi) *phi = h->m.phi;

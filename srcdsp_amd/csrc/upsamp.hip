@@ -27,6 +27,7 @@ struct srcdsp_up_state {
     unsigned length = 0;
     int left_shift_factor = 0;
     int32_t *d_coef = nullptr;  // polyphase order: d_coef[o*H + i] = c[o + i*L]
+    bool coef_i24 = false;      // every tap in (-2^23, 2^23): v_mad_i32_i24
     void *d_hist[2] = {nullptr, nullptr};
     size_t hist_cap = 0;
     int cur = 0;
@@ -87,6 +88,120 @@ __global__ __launch_bounds__(256) void up_kernel(const void *in, long n_in, long
     }
 }
 
+// Tiled polyphase interpolator for complex<int16_t> input (UV_CI16_I32 /
+// UV_CI16_I16), ratio LR in {2, 4, 8} (template), H = ntaps / L taps per phase
+// (runtime).  Each lane owns R = 4 consecutive input samples (4L outputs) and
+// keeps a 8-sample register window as two 4-sample blocks lo|hi that rotate
+// roles every 4 taps (tap i of input r reads sample r - i); the L phases share
+// each window sample.  Taps are wave-uniform SGPR operands (polyphase order:
+// coef[o*H + i]).  The tile's input span (1024 samples + H-1 halo rounded to
+// 4) is staged through LDS as packed words; lanes read whole 16-B granules at
+// granule stride 1 (conflict-free).  Products: v_mad_i32_i24 when the host
+// has checked |c| < 2^23 (I24), exact 32-bit multiply otherwise; the int16
+// variant wraps each product to int16 (std::operator*, UV_CI16_I16).
+constexpr int kUpR = 4, kUpBlock = 256, kUpMaxTaps = 4096;
+
+template <int UV, int LR, bool I24>
+__global__ __launch_bounds__(kUpBlock) void up_tile(const uint32_t *in, long n_in, long n_total,
+                                                    const uint32_t *hist_in, uint32_t *hist_out,
+                                                    const int32_t *coef, int H, unsigned shift, uint32_t *out) {
+    constexpr int R = kUpR, TI = R * kUpBlock;
+    extern __shared__ uint4 ug[];
+    const int Hm1 = H - 1;
+    const int NQ = (H + 3) / 4;
+    const int P0 = 4 * NQ;  // halo samples staged in front of the tile (>= H-1, block aligned)
+    const int t = threadIdx.x;
+    if (blockIdx.x == 0) {
+        for (int k = t; k < Hm1; k += kUpBlock) {
+            const long j = n_total - Hm1 + k;
+            hist_out[k] = up_fetch<UV>(in, hist_in, j, n_in, Hm1);
+        }
+    }
+    const long j0 = (long)blockIdx.x * TI;
+    const int ng = (TI + P0) / 4;
+    for (int g = t; g < ng; g += kUpBlock) {
+        const long s0 = j0 - P0 + 4L * g;
+        uint4 v;
+        if (s0 >= 0 && s0 + 4 <= n_in) {
+            v = *(const uint4 *)(in + s0);
+        } else {
+            v = make_uint4(up_fetch<UV>(in, hist_in, s0, n_in, Hm1), up_fetch<UV>(in, hist_in, s0 + 1, n_in, Hm1),
+                           up_fetch<UV>(in, hist_in, s0 + 2, n_in, Hm1), up_fetch<UV>(in, hist_in, s0 + 3, n_in, Hm1));
+        }
+        ug[g] = v;
+    }
+    __syncthreads();
+    const int gb = NQ + t;  // lane's first granule (sample P0 + 4t)
+    int32_t xr_lo[4], xi_lo[4], xr_hi[4], xi_hi[4];
+    auto fill = [&](int32_t (&dr)[4], int32_t (&di)[4], int c) {
+        const uint4 v = ug[gb + c];
+        dr[0] = sext16(v.x); di[0] = sext16_hi(v.x);
+        dr[1] = sext16(v.y); di[1] = sext16_hi(v.y);
+        dr[2] = sext16(v.z); di[2] = sext16_hi(v.z);
+        dr[3] = sext16(v.w); di[3] = sext16_hi(v.w);
+    };
+    uint32_t yr[LR][R], yi[LR][R];
+#pragma unroll
+    for (int o = 0; o < LR; ++o)
+#pragma unroll
+        for (int r = 0; r < R; ++r) yr[o][r] = yi[o][r] = 0;
+    ConstPtr<int32_t> tp = const_view<int32_t>(coef);
+    auto mac = [&](int32_t c, int32_t x) -> uint32_t {
+        uint32_t p = I24 ? (uint32_t)__mul24(c, x) : (uint32_t)c * (uint32_t)x;
+        if constexpr (UV == UV_CI16_I16) p = (uint32_t)sext16(p);
+        return p;
+    };
+    // chunk q (taps 4q..4q+3): input r reads sample r - i, i.e. block lo
+    // (samples -4q-4..-4q-1) or hi (-4q..-4q+3)
+    auto chunk = [&](int q, const int32_t (&lr)[4], const int32_t (&li)[4], const int32_t (&hr)[4],
+                     const int32_t (&hi)[4], bool guard) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int i = 4 * q + p;
+            if (guard && i >= H) break;
+            int32_t c[LR];
+#pragma unroll
+            for (int o = 0; o < LR; ++o) c[o] = tp[o * H + i];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int rel = r - p + 4;  // 1..7 over lo|hi
+                const int32_t xr = rel < 4 ? lr[rel] : hr[rel - 4];
+                const int32_t xi = rel < 4 ? li[rel] : hi[rel - 4];
+#pragma unroll
+                for (int o = 0; o < LR; ++o) {
+                    yr[o][r] += mac(c[o], xr);
+                    yi[o][r] += mac(c[o], xi);
+                }
+            }
+        }
+    };
+    int32_t ar[4], ai[4], br[4], bi[4];
+    fill(br, bi, 0);  // hi block of chunk 0
+    int q = 0;
+    for (; q + 2 <= NQ; q += 2) {
+        asm volatile("" : "+s"(tp));
+        fill(ar, ai, -q - 1);
+        chunk(q, ar, ai, br, bi, false);
+        fill(br, bi, -q - 2);
+        chunk(q + 1, br, bi, ar, ai, q + 2 == NQ);
+    }
+    if (q < NQ) {
+        fill(ar, ai, -q - 1);
+        chunk(q, ar, ai, br, bi, true);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const long j = j0 + 4L * t + r;
+        if (j >= n_total) break;
+        uint32_t w[LR];
+#pragma unroll
+        for (int o = 0; o < LR; ++o) w[o] = pack16(limit_t16((int32_t)yr[o][r], shift), limit_t16((int32_t)yi[o][r], shift));
+        uint32_t *dst = out + (long)LR * j;
+#pragma unroll
+        for (int o = 0; o < LR; o += 2) *(uint2 *)(dst + o) = make_uint2(w[o], w[o + 1]);
+    }
+}
+
 static int in_bytes(int v) { return v == UV_I16_I32 ? 2 : 4; }
 
 static int up_set(srcdsp_up_state &u, const void *coeffs, int n) {
@@ -107,6 +222,8 @@ static int up_set(srcdsp_up_state &u, const void *coeffs, int n) {
         return SRCDSP_ERR_ARG;
     }
     const int H = n / (int)u.L;
+    u.coef_i24 = true;
+    for (int i = 0; i < n; ++i) u.coef_i24 = u.coef_i24 && c[i] < (1 << 23) && c[i] >= -(1 << 23);
     std::vector<int32_t> poly((size_t)n);
     for (unsigned o = 0; o < u.L; ++o)
         for (int i = 0; i < H; ++i) poly[o * H + i] = c[o + i * u.L];
@@ -148,6 +265,40 @@ static int up_launch(srcdsp_up_state &u, const void *d_in, size_t n_in, void *d_
     int rc = u.order.before(s);
     if (rc) return rc;
     const unsigned shift = iter ? 0u : (unsigned)(15 - u.left_shift_factor);
+    const void *hin0 = u.d_hist[u.cur];
+    void *hout0 = u.d_hist[u.cur ^ 1];
+    const bool tiled = u.variant != UV_I16_I32 && (u.L == 2 || u.L == 4 || u.L == 8) && u.ntaps <= kUpMaxTaps &&
+                       ((uintptr_t)d_in & 15u) == 0 && ((uintptr_t)d_out & 7u) == 0;
+    if (tiled) {
+        constexpr int TI = kUpR * kUpBlock;
+        const int NQ = (u.H + 3) / 4;
+        const size_t smem = 16 * (size_t)((TI + 4 * NQ) / 4);
+        const dim3 grid((unsigned)((n_total + TI - 1) / TI));
+        const uint32_t *i32 = (const uint32_t *)d_in;
+        const uint32_t *h32 = (const uint32_t *)hin0;
+        uint32_t *ho32 = (uint32_t *)hout0, *o32 = (uint32_t *)d_out;
+#define SRCDSP_UP_TILE(UVV, LL, I24)                                                                             \
+    hipLaunchKernelGGL((up_tile<UVV, LL, I24>), grid, dim3(kUpBlock), smem, s, i32, (long)n_in, n_total, h32, ho32, \
+                       u.d_coef, u.H, shift, o32)
+#define SRCDSP_UP_L(UVV, I24)                 \
+    switch (u.L) {                             \
+    case 2: SRCDSP_UP_TILE(UVV, 2, I24); break; \
+    case 4: SRCDSP_UP_TILE(UVV, 4, I24); break; \
+    default: SRCDSP_UP_TILE(UVV, 8, I24); break; \
+    }
+        if (u.variant == UV_CI16_I16) {
+            SRCDSP_UP_L(UV_CI16_I16, true)  // int16 taps always fit i24
+        } else if (u.coef_i24) {
+            SRCDSP_UP_L(UV_CI16_I32, true)
+        } else {
+            SRCDSP_UP_L(UV_CI16_I32, false)
+        }
+#undef SRCDSP_UP_L
+#undef SRCDSP_UP_TILE
+        SRCDSP_HIP_TRY(hipGetLastError());
+        u.cur ^= 1;
+        return u.order.after(s);
+    }
     const int blocks = (int)std::max<long>(1, std::min<long>((n_total + 255) / 256, 4096));
     const size_t smem = 4 * (size_t)u.ntaps;
     const void *hin = u.d_hist[u.cur];

@@ -319,6 +319,16 @@ class Mixer(_Handle):
 
     set_frequency, adjust_frequency = setFrequency, adjustFrequency
 
+    def setPhase(self, phi: int):
+        """Not a reference method: set the phase accumulator, e.g.
+        to phaseAt(k) for a buffer segment starting at sample k."""
+        A.call("srcdsp_mixer_set_phase", self._h, int(phi))
+
+    def phaseAt(self, k: int) -> int:
+        """Closed form of mixers.h:177: the phase after k samples from now."""
+        phi, freq = self.state()[:2]
+        return (phi + (k % self.N) * freq) % self.N
+
     def state(self):
         p, fr, nom = C.c_int(), C.c_int(), C.c_float()
         A.call("srcdsp_mixer_get_state", self._h, C.byref(p), C.byref(fr), C.byref(nom))
@@ -393,6 +403,14 @@ class FixedPatternCorrelator(_Handle):
             x = _host(inp, "ci16")
             A.call("srcdsp_corr_step_host", self._h, _ptr(x), n, C.byref(found), C.byref(idx))
         return bool(found.value), idx.value
+
+    def prime(self, inp):
+        """Not a reference method: leave the state step() would
+        leave after streaming `inp` with no detection test -- seeds a time
+        segment of a split buffer with its halo.  Device input only."""
+        if not _is_device(inp):
+            raise TypeError("prime() takes a device-resident buffer")
+        A.call("srcdsp_corr_prime", self._h, _ptr(inp), _nsamples(inp, "ci16"), _stream(inp))
 
     def getRefBitSamples(self):
         b = np.zeros((self.N, 2), np.int16)

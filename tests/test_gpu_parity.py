@@ -157,6 +157,30 @@ def test_mixdecim_chain_table_sizes(S, O, N, f):
         assert m.state()[:2] == om.state()[:2]
 
 
+@pytest.mark.parametrize("fp", ["fma", "strict"])
+@pytest.mark.parametrize("ntaps", [1, 2, 3, 5, 12, 13, 31, 127, 1000, 1030])
+def test_fir_float_tile_kernel_vs_oracle(S, O, fp, ntaps):
+    """FilterFir<cf32,cf32,cf32,float> and <float,cf32,float,float>: the
+    single-rate tile kernel (runtime tap count <= 1024; 1030 takes the generic
+    kernel), chained calls of uneven length, bit-exact per float contract."""
+    rng = np.random.default_rng(ntaps)
+    c = (rng.standard_normal(ntaps) / max(4, ntaps)).astype(np.float32)
+    xc = O[fp].gen_cf32(21, 0, 0, 70001)
+    xr = np.ascontiguousarray(xc.view(np.float32)[:, 0]) if xc.ndim == 2 else xc.real.astype(np.float32)
+    for kind in ("cf32", "f32"):
+        if kind == "cf32":
+            g = S.FilterFir(c, fp=fp)
+            r = O[fp].fir(0, c)
+            x = xc
+        else:
+            g = S.FilterFir(c, "float", "complex<float>", "float", "float", fp=fp)
+            r = O[fp].fir(1, c)
+            x = xr
+        for off, n in _chunks(len(x), [16384, 3, 4096 + 8, 40000, 1]):
+            xs = x[off:off + n]
+            assert np.array_equal(g.step(dev(xs)).cpu().numpy(), r.step(xs)), (kind, off, n)
+
+
 def test_decim_batched_equals_single(S, O):
     import torch
     from srcdsp_amd.design import hamming_sinc
@@ -266,6 +290,37 @@ def test_upsampler_vs_oracle(S, O):
             assert np.array_equal(g.step(dev(xs), None, last, it).cpu().numpy(), r.step(xs, last, it)), (it, off)
 
 
+_UP_TYPES = {0: ("complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int32_t"),
+             1: ("complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int16_t"),
+             2: ("int16_t", "int16_t", "int32_t", "int32_t")}
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("L,H", [(2, 1), (2, 7), (4, 32), (4, 33), (8, 16), (3, 5), (4, 2000)])
+def test_upsampler_tile_kernel_vs_oracle(S, O, variant, L, H):
+    """Tiled interpolator (L in 2/4/8, <= 4096 taps) and the generic one (other
+    L, int16 input, longer filters): flush and iterator overloads, wide taps
+    (|c| >= 2^23 takes the exact 32-bit multiply), int16 product wrap."""
+    rng = np.random.default_rng(L * 1000 + H + 7 * variant)
+    n = L * H
+    lim = {0: 1 << 24, 1: 32767, 2: 20000}[variant]
+    c = rng.integers(-lim, lim + 1, size=n)
+    c[-1] = 0  # trailing zero tap: length < ImpLength (upsampling_filters.h:121-123)
+    c[0] = lim
+    x = O["fma"].gen_ci16(L + H, variant, 0, 50000, -32768, 32767)
+    if variant == 2:
+        x = np.ascontiguousarray(x[:, 0]) if x.ndim == 2 else x
+    g = S.FilterUpsamplingFir(c, L, *_UP_TYPES[variant])
+    r = O["fma"].up(variant, L, c)
+    for it in (False, True):
+        for off, m in _chunks(len(x), [20000, 1, 4099, 30000]):
+            xs = x[off:off + m]
+            last = off + m >= len(x)
+            assert np.array_equal(g.step(dev(xs), None, last, it).cpu().numpy(), r.step(xs, last, it)), (it, off)
+        g.reset()
+        r.reset()
+
+
 @pytest.mark.parametrize("N,S_", [(1024, 1), (32, 4), (64, 2)])
 def test_correlator_vs_oracle(S, O, N, S_):
     from srcdsp_amd.design import qpsk_pattern
@@ -293,3 +348,69 @@ def test_correlator_vs_oracle(S, O, N, S_):
         events += fr
         pos += (ir + 2) if fr else len(xs)
     assert events >= 1
+
+
+def test_time_split_segments_equal_single_call(S, O):
+    """SURVEY 8e, one long buffer split in time (W = 3 segments run one after
+    another here, as 3 ranks would): decimator seeded by stepping its halo,
+    mixer by setPhase(phaseAt(start)), correlator by prime(); outputs and the
+    first detection are bit-identical to the unsplit call."""
+    import torch
+    from srcdsp_amd import dist as D
+    from srcdsp_amd.design import hamming_sinc, q14, qpsk_pattern
+    W = 3
+    # decimator (cf32)
+    c = hamming_sinc(127)
+    x = dev(O["fma"].gen_cf32(0x5EED, 0, 0, 3 * 65536 + 12))
+    ref = S.FilterDnsamplingFir(c, 4).step(x).cpu().numpy()
+    parts = []
+    for r in range(W):
+        s0, s1 = D.time_segment(x.shape[0], W, r, align=4)
+        h = min(s0, D.decim_halo(127, 4))
+        parts.append(S.FilterDnsamplingFir(c, 4).step(x[s0 - h:s1].contiguous())[h // 4:].cpu().numpy())
+    assert np.array_equal(np.concatenate(parts), ref)
+    # mixer -> decimator chain (ci16): mixer phase in closed form at the halo start
+    cq = q14(hamming_sinc(127))
+    xi = dev(O["fma"].gen_ci16(0x5EED, 1, 0, 3 * 65536 + 12, -32768, 32767))
+    dtypes = ("complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int32_t")
+
+    def chain(f):
+        m = S.Mixer(4096)
+        m.reset(f)
+        return m, S.MixerDecimatorChain(m, S.FilterDnsamplingFir(cq, 4, *dtypes))
+
+    m0, ch0 = chain(0.1)
+    ref = ch0.step(xi).cpu().numpy()
+    parts = []
+    for r in range(W):
+        s0, s1 = D.time_segment(xi.shape[0], W, r, align=4)
+        h = min(s0, D.decim_halo(127, 4))
+        m, ch = chain(0.1)
+        m.setPhase(m.phaseAt(s0 - h))
+        parts.append(ch.step(xi[s0 - h:s1].contiguous())[h // 4:].cpu().numpy())
+    assert np.array_equal(np.concatenate(parts), ref)
+    # correlator: pattern straddling a segment boundary, and inside segment 2
+    p = qpsk_pattern(1024, 500, seed=2)
+    rng = np.random.default_rng(3)
+    for where in (None, 200000 - 500, 300000):
+        xc = rng.integers(-125, 126, size=(400000, 2))
+        if where is not None:
+            xc[where:where + 1024] += 2 * p
+        xd = dev(xc.astype(np.int16))
+        g = S.FixedPatternCorrelator(1024, 1)
+        g.setPattern(p)
+        found, idx = g.step(xd)
+        bits = g.getRefBitSamples()
+        first, owner = D.NO_DETECTION, None
+        for r in range(W):
+            s0, s1 = D.time_segment(xd.shape[0], W, r)
+            hc = min(s0, D.corr_halo(1024, 1))
+            gr = S.FixedPatternCorrelator(1024, 1)
+            gr.setPattern(p)
+            loc = D.corr_segment_search(gr, xd[s0 - hc:s0].contiguous() if hc else None, xd[s0:s1].contiguous(), s0)
+            if loc is not None and loc < first:
+                first, owner = loc, gr
+        assert (found, idx if found else D.NO_DETECTION) == (where is not None, first)
+        if found:
+            assert np.array_equal(owner.getRefBitSamples(), bits)
+    del torch
