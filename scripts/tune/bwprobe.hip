@@ -66,6 +66,35 @@ __global__ __launch_bounds__(256) void rw_probe(const float4_t *in, float4_t *ou
         if (acc.x == 1234.5f) out[0] = acc;
 }
 
+// 4:1 contiguous-per-block stream through buffer intrinsics with explicit
+// cache-policy bits (gfx950 aux: bit0 sc0, bit1 nt, bit4 sc1) on loads / stores
+template <int LA, int SA>
+__global__ __launch_bounds__(256) void aux_probe(const float4_t *in, float4_t *out, long n_out) {
+    const int t = threadIdx.x;
+    const long per = (n_out + gridDim.x - 1) / gridDim.x;
+    const long begin = blockIdx.x * per;
+    const long end = begin + per < n_out ? begin + per : n_out;
+    __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc((void *)(in + 4 * begin), 0, 0x7ffffff0, 0x00020000);
+    __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void *)(out + begin), 0, 0x7ffffff0, 0x00020000);
+    for (long base = 0; begin + base + 512 <= end; base += 512) {
+        float4_t v[8];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const long ow = base + u * 256 + (t & ~63);
+                auto w = __builtin_amdgcn_raw_buffer_load_b128(ri, (int)(16 * (4 * ow + r * 64 + (t & 63))), 0, LA);
+                v[u * 4 + r] = __builtin_bit_cast(float4_t, w);
+            }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            float4_t s = v[u * 4] + v[u * 4 + 1] + v[u * 4 + 2] + v[u * 4 + 3];
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b128(ri, 0, 0, 0)), s),
+                                                   ro, (int)(16 * (base + u * 256 + t)), 0, SA);
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void fill_probe(float4_t *out, long n) {
     const long nth = (long)gridDim.x * 256;
     const float4_t z = {1, 2, 3, 4};
@@ -96,6 +125,15 @@ extern "C" int bw_probe(int id, int blocks, const void *in_, void *out_, long n_
         CASE(10, 0, 2, true, false, false)  // read only nt
         CASE(11, 4, 4, false, false, false) // 4:1, 16 loads in flight
         CASE(12, 1, 2, false, true, false)  // copy nt stores
+#define ACASE(id, LA, SA)                                                                          \
+    case id:                                                                                        \
+        hipLaunchKernelGGL((aux_probe<LA, SA>), dim3(blocks), dim3(256), 0, s, in, out, n_in16 / 4); \
+        break;
+        ACASE(100, 0, 0) ACASE(101, 0, 1) ACASE(102, 0, 2) ACASE(103, 0, 3) ACASE(104, 0, 16) ACASE(105, 0, 17)
+        ACASE(106, 0, 18) ACASE(107, 0, 19)
+        ACASE(110, 2, 0) ACASE(111, 2, 1) ACASE(112, 2, 2) ACASE(113, 2, 3) ACASE(114, 2, 16) ACASE(115, 2, 17)
+        ACASE(116, 2, 18) ACASE(117, 2, 19)
+        ACASE(120, 1, 2) ACASE(121, 3, 2) ACASE(122, 16, 2) ACASE(123, 17, 2) ACASE(124, 18, 2) ACASE(125, 19, 2)
     case 20:
         hipLaunchKernelGGL(fill_probe, dim3(blocks), dim3(256), 0, s, out, n_in16 / 4);
         break;

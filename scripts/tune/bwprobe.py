@@ -27,6 +27,14 @@ def main():
     sp = C.c_void_p(st.cuda_stream)
     res = {}
     grids = (1024, 2048, 4096, 8192)
+    if os.environ.get("BW_AUX"):
+        CASES.clear()
+        for la in (0, 2):
+            for k, sa in enumerate((0, 1, 2, 3, 16, 17, 18, 19)):
+                CASES[100 + 10 * (la // 2) + k] = (f"4:1 contig ld aux {la} st aux {sa}", 4)
+        for k, la in enumerate((1, 3, 16, 17, 18, 19)):
+            CASES[120 + k] = (f"4:1 contig ld aux {la} st aux 2", 4)
+        grids = (1024, 2048)
     for rnd in range(4):
         for cid in CASES:
             for g in grids:
