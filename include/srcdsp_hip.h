@@ -206,6 +206,56 @@ SRCDSP_API int srcdsp_corr_get_status(srcdsp_corr_t h, uint32_t *energy3, uint32
                                       uint32_t *coeffs_energy, int *coeff_scaling,
                                       double *threshold_factor);
 
+/* ============================================================================
+ * FifoWithTimeTrack<T, N>   (buffers.h:58-459), the ring in HBM
+ * One producer thread writes, one consumer thread reads (as the reference).
+ * Element type T is opaque: elem_bytes per element.
+ * ==========================================================================*/
+typedef struct srcdsp_fifo *srcdsp_fifo_t;
+/* ctor FifoWithTimeTrack(samplingFrequency)  buffers.h:62-66 (storage(N) zeroed) */
+SRCDSP_API int srcdsp_fifo_create(srcdsp_fifo_t *out, size_t elem_bytes, size_t N, double sampling_frequency);
+SRCDSP_API int srcdsp_fifo_destroy(srcdsp_fifo_t h);
+/* write(in, seconds, fracSeconds)  buffers.h:140-224.  Host input, staged
+ * through two pinned buffers; returns before its H2D copy completes (readers
+ * are ordered after it on the device).  assert(inSize < N) -> SRCDSP_ERR_SIZE. */
+SRCDSP_API int srcdsp_fifo_write(srcdsp_fifo_t h, const void *in, size_t n, unsigned seconds,
+                                 double frac_seconds);
+/* the same for device-resident input, copied D2D on `stream` */
+SRCDSP_API int srcdsp_fifo_write_device(srcdsp_fifo_t h, const void *d_in, size_t n, unsigned seconds,
+                                        double frac_seconds, void *stream);
+/* read(out, start) -> bool  buffers.h:282-349.  *error = the reference's return
+ * value (1: range not available); *start is raised to timeStart as the
+ * reference does (with its stderr warning).  Output in device memory, copied
+ * on `stream`; assert(out.size() != 0) -> SRCDSP_ERR_SIZE. */
+SRCDSP_API int srcdsp_fifo_read(srcdsp_fifo_t h, void *d_out, size_t n, uint64_t *start, int *error,
+                                void *stream);
+SRCDSP_API int srcdsp_fifo_read_host(srcdsp_fifo_t h, void *out, size_t n, uint64_t *start, int *error);
+/* count()  buffers.h:377-392 ; reset()  buffers.h:245-258 (indices only) */
+SRCDSP_API int srcdsp_fifo_count(srcdsp_fifo_t h, size_t *count);
+SRCDSP_API int srcdsp_fifo_reset(srcdsp_fifo_t h);
+/* the fields dumpInfo() prints  buffers.h:229-240 */
+SRCDSP_API int srcdsp_fifo_get_state(srcdsp_fifo_t h, size_t *write_ptr, uint64_t *time_start,
+                                     uint64_t *time_end, int *rollover);
+/* getAbsoluteTime(timePoint, fracTimePoint)  buffers.h:413-459 */
+SRCDSP_API int srcdsp_fifo_get_absolute_time(srcdsp_fifo_t h, uint64_t time_point, double frac_time_point,
+                                             unsigned *seconds, double *frac_seconds);
+
+/* ============================================================================
+ * Binary I/Q captures   (dsptl_files.h:101-109 saveBinarySamples,
+ * :250-262 readBinarySamples).  Interleaved I,Q components of
+ * component_bytes each.  Reading returns whole samples only and replaces the
+ * output (the reference's out.empty() / trailing-sample bugs fixed).
+ * ==========================================================================*/
+SRCDSP_API int srcdsp_iq_save(const char *path, const void *d_samples, size_t n, size_t component_bytes,
+                              int append, void *stream);
+SRCDSP_API int srcdsp_iq_save_host(const char *path, const void *samples, size_t n, size_t component_bytes,
+                                   int append);
+/* number of whole samples in the file */
+SRCDSP_API int srcdsp_iq_count(const char *path, size_t component_bytes, size_t *n);
+SRCDSP_API int srcdsp_iq_load(const char *path, size_t component_bytes, void *d_out, size_t cap, size_t *n,
+                              void *stream);
+SRCDSP_API int srcdsp_iq_load_host(const char *path, size_t component_bytes, void *out, size_t cap, size_t *n);
+
 /* ---------------------------------------------------------------- misc */
 /* Last error text of the calling thread (HIP error string or argument check). */
 SRCDSP_API const char *srcdsp_last_error(void);

@@ -129,7 +129,19 @@ class Oracle:
             "corr_destroy": _sig(lib, "orc_corr_destroy", None, VP),
             "gen_cf32": _sig(lib, "orc_gen_cf32", None, C.c_uint64, C.c_uint64, C.c_uint64, L, I, I, VP),
             "gen_ci16": _sig(lib, "orc_gen_ci16", None, C.c_uint64, C.c_uint64, C.c_uint64, L, I, I, VP),
+            "fifo_create": _sig(lib, "orc_fifo_create", VP, C.c_size_t, C.c_size_t, D),
+            "fifo_write": _sig(lib, "orc_fifo_write", I, VP, VP, C.c_size_t, U, D),
+            "fifo_read": _sig(lib, "orc_fifo_read", I, VP, VP, C.c_size_t, VP),
+            "fifo_count": _sig(lib, "orc_fifo_count", C.c_size_t, VP),
+            "fifo_reset": _sig(lib, "orc_fifo_reset", None, VP),
+            "fifo_abs": _sig(lib, "orc_fifo_absolute_time", None, VP, C.c_uint64, D, VP, VP),
+            "fifo_destroy": _sig(lib, "orc_fifo_destroy", None, VP),
         }
+
+    def fifo(self, dtype, N, sampling_frequency=0.0):
+        """FifoWithTimeTrack<T, N> restated (buffers.h:58-459); dtype = numpy
+        dtype of one element (e.g. complex<int16_t> -> ("<i2", 2) rows)."""
+        return _Fifo(self, np.dtype(dtype), N, sampling_frequency)
 
     # factories --------------------------------------------------------------
     def decim(self, variant, M, coeffs, abs_mode=None):
@@ -299,6 +311,37 @@ class _Corr(_Handle):
                 "coeff_scaling": cs.value, "threshold_factor": tf.value}
 
 
+class _Fifo(_Handle):
+    """Common Python face of the FIFO restatement and the reference build."""
+
+    def __init__(self, o, dtype, N, fs):
+        self.o, self.dtype, self.N = o, dtype, N
+        super().__init__(o.f["fifo_create"](dtype.itemsize, N, fs), o.f["fifo_destroy"])
+
+    def write(self, x, seconds=0, frac_seconds=0.0):
+        x = np.ascontiguousarray(x)  # raw element bytes (a subarray dtype would broadcast)
+        assert x.nbytes % self.dtype.itemsize == 0
+        return self.o.f["fifo_write"](self._h, _ptr(x), x.nbytes // self.dtype.itemsize, seconds, frac_seconds)
+
+    def read(self, n, start):
+        """-> (error flag as the reference's bool, start after the call, data)"""
+        out = np.zeros(n, self.dtype)
+        st = C.c_uint64(start)
+        err = self.o.f["fifo_read"](self._h, _ptr(out), n, C.byref(st))
+        return err, st.value, out
+
+    def count(self):
+        return int(self.o.f["fifo_count"](self._h))
+
+    def reset(self):
+        self.o.f["fifo_reset"](self._h)
+
+    def absolute_time(self, time_point, frac=0.0):
+        sec, fs = C.c_uint(), C.c_double()
+        self.o.f["fifo_abs"](self._h, time_point, frac, C.byref(sec), C.byref(fs))
+        return sec.value, fs.value
+
+
 # ----------------------------------------------------------------------------
 # real reference (oracle/_ref)
 # ----------------------------------------------------------------------------
@@ -462,3 +505,76 @@ class _RefCorr(_Corr):
         self.o, self.N, self.S = r, N, S
         h = r.f["corr_create"](N, S)
         _Handle.__init__(self, h, r.f["corr_destroy"])
+
+
+# ------------------------------------------------ reference buffers.h / files
+class ReferenceIO:
+    """buffers.h FifoWithTimeTrack and dsptl_files.h binary I/Q functions of
+    the reference build (oracle/_ref/<flavour>/libref_io.so)."""
+    KINDS = {("<f8", 15): 0, ("<i2", 64): 1, ("<i2", 1000): 2}
+
+    def __init__(self, flavour: str = "strict"):
+        lib = C.CDLL(os.path.join(HERE, "_ref", flavour, "libref_io.so"))
+        self.f = {
+            "create": _sig(lib, "ref_fifo_create", VP, I, D),
+            "write": _sig(lib, "ref_fifo_write", None, VP, VP, L, U, D),
+            "read": _sig(lib, "ref_fifo_read", I, VP, VP, L, VP),
+            "count": _sig(lib, "ref_fifo_count", C.c_ulong, VP),
+            "reset": _sig(lib, "ref_fifo_reset", None, VP),
+            "abs": _sig(lib, "ref_fifo_abs_time", None, VP, C.c_uint64, D, VP, VP),
+            "destroy": _sig(lib, "ref_fifo_destroy", None, VP),
+            "iq_save": _sig(lib, "ref_iq_save", None, C.c_char_p, I, VP, L),
+            "iq_read": _sig(lib, "ref_iq_read", L, C.c_char_p, I, VP, L),
+        }
+
+    def fifo(self, kind: int, fs: float = 0.0):
+        """kind 0: <double, 15>, 1: <complex<int16_t>, 64>, 2: <complex<int16_t>, 1000>"""
+        return _RefFifo(self, kind, fs)
+
+    def iq_save(self, path: str, x: np.ndarray):
+        x = np.ascontiguousarray(x)
+        t = 0 if x.dtype == np.int16 else 1
+        self.f["iq_save"](path.encode(), t, _ptr(x), x.shape[0])
+
+    def iq_read(self, path: str, component_dtype, cap: int = 1 << 22):
+        t = 0 if np.dtype(component_dtype) == np.int16 else 1
+        out = np.zeros((cap, 2), component_dtype)
+        n = self.f["iq_read"](path.encode(), t, _ptr(out), cap)
+        return out[:min(n, cap)], n
+
+
+class _RefFifo:
+    def __init__(self, r, kind, fs):
+        self.r, self.kind = r, kind
+        self.dtype, self.N = ((np.dtype("<f8"), 15), (np.dtype(("<i2", 2)), 64), (np.dtype(("<i2", 2)), 1000))[kind]
+        self._h = r.f["create"](kind, fs)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self.r.f["destroy"](self._h)
+            self._h = None
+
+    def write(self, x, seconds=0, frac_seconds=0.0):
+        x = np.ascontiguousarray(x)  # raw element bytes (a subarray dtype would broadcast)
+        n = x.nbytes // self.dtype.itemsize
+        assert n * self.dtype.itemsize == x.nbytes and n < self.N, "the reference asserts inSize < N"
+        self.r.f["write"](self._h, _ptr(x), n, seconds, frac_seconds)
+        return 0
+
+    def read(self, n, start):
+        assert n > 0, "the reference asserts out.size() != 0"
+        out = np.zeros(n, self.dtype)
+        st = C.c_uint64(start)
+        err = self.r.f["read"](self._h, _ptr(out), n, C.byref(st))
+        return err, st.value, out
+
+    def count(self):
+        return int(self.r.f["count"](self._h))
+
+    def reset(self):
+        self.r.f["reset"](self._h)
+
+    def absolute_time(self, time_point, frac=0.0):
+        sec, fs = C.c_uint(), C.c_double()
+        self.r.f["abs"](self._h, time_point, frac, C.byref(sec), C.byref(fs))
+        return sec.value, fs.value

@@ -649,3 +649,119 @@ void orc_gen_ci16(uint64_t seed, uint64_t ch, uint64_t off, long n, int lo, int 
     uint64_t key = seed ^ (ch << 40);
     for (long i = 0; i < 2 * n; ++i) out[i] = (int16_t)gen_val(key, 2 * off + (uint64_t)i, lo, hi);
 }
+
+
+/* ===================================================== FifoWithTimeTrack
+ * buffers.h:58-459.  Bookkeeping restated with the reference's uint64/size_t
+ * modular arithmetic, including its quirks: timeStart = 1 while the ring is
+ * not full (:199-202), count() = timeEnd - timeStart + 1 (so 1 when empty,
+ * :377-392), reset() clears the indices only (:245-258).                  */
+struct orc_fifo {
+    size_t es, N;
+    unsigned char *storage;
+    size_t write_ptr;
+    uint64_t time_start, time_end;
+    int rollover;
+    double fs;
+    uint64_t ref_tp;
+    unsigned ref_sec;
+    double ref_frac;
+};
+
+orc_fifo *orc_fifo_create(size_t elem_bytes, size_t N, double fs) {
+    orc_fifo *f = (orc_fifo *)calloc(1, sizeof(orc_fifo));
+    f->es = elem_bytes;
+    f->N = N;
+    f->storage = (unsigned char *)calloc(N, elem_bytes); /* storage(N): value-initialised */
+    f->fs = fs;
+    return f;
+}
+
+int orc_fifo_write(orc_fifo *f, const void *in, size_t n, unsigned seconds, double frac) {
+    const size_t N = f->N, es = f->es;
+    if (n >= N) return -1; /* assert(inSize < N) :145 */
+    const size_t up = N - f->write_ptr;
+    const unsigned char *src = (const unsigned char *)in;
+    if (n <= up) {
+        memcpy(f->storage + f->write_ptr * es, src, n * es);
+    } else {
+        memcpy(f->storage + f->write_ptr * es, src, up * es);
+        memcpy(f->storage, src + up * es, (n - up) * es);
+    }
+    f->write_ptr = (f->write_ptr + n) % N; /* :162 */
+    uint64_t diff = UINT64_MAX - f->time_end;
+    f->ref_tp = f->time_end + 1; /* :171-173 */
+    f->ref_sec = seconds;
+    f->ref_frac = frac;
+    if (diff >= n) {
+        f->time_end += n;
+    } else {
+        f->time_end = n - diff;
+        f->rollover = 1;
+    }
+    if (!f->rollover) { /* :192-202 */
+        if ((f->time_end - f->time_start + 1) > N)
+            f->time_start = f->time_end - N + 1;
+        else
+            f->time_start = 1;
+    } else {
+        uint64_t d2 = UINT64_MAX - f->time_start;
+        if (d2 >= n)
+            f->time_start += n;
+        else
+            f->time_start = n - d2;
+        f->rollover = 0;
+    }
+    return 0;
+}
+
+int orc_fifo_read(orc_fifo *f, void *out, size_t n, uint64_t *start) {
+    const size_t N = f->N, es = f->es;
+    if (n == 0) return -1; /* assert(out.size() != 0) :286 */
+    if (*start < f->time_start) *start = f->time_start; /* :299-305 (warning on stderr) */
+    if ((*start + n - 1) > f->time_end) return 1;
+    uint64_t end = *start + n - 1;
+    size_t sp = (size_t)((f->write_ptr + N - (f->time_end - *start) - 1) % N); /* :313-314 */
+    size_t ep = (size_t)((f->write_ptr + N - (f->time_end - end) - 1) % N);
+    unsigned char *dst = (unsigned char *)out;
+    if (ep >= sp) {
+        memcpy(dst, f->storage + sp * es, (ep + 1 - sp) * es);
+    } else {
+        memcpy(dst, f->storage + sp * es, (N - sp) * es);
+        memcpy(dst + (N - sp) * es, f->storage, (ep + 1) * es);
+    }
+    return 0;
+}
+
+size_t orc_fifo_count(const orc_fifo *f) {
+    if (!f->rollover) return (size_t)((f->time_end - f->time_start) + 1);
+    return (size_t)((UINT64_MAX - f->time_start) + f->time_end + 1);
+}
+
+void orc_fifo_reset(orc_fifo *f) {
+    f->write_ptr = 0;
+    f->time_start = 0;
+    f->time_end = 0;
+    f->rollover = 0;
+}
+
+/* buffers.h:413-459 */
+void orc_fifo_absolute_time(const orc_fifo *f, uint64_t tp, double frac_tp, unsigned *seconds, double *frac_seconds) {
+    int64_t sample_diff = (int64_t)(tp - f->ref_tp);
+    double time_diff = sample_diff / f->fs;
+    int32_t tdi = (int32_t)floor(time_diff);
+    double tdf = time_diff - floor(time_diff);
+    uint32_t sec = f->ref_sec + tdi;
+    double fs = f->ref_frac + tdf + (frac_tp / f->fs);
+    int32_t tmp = (int32_t)fs;
+    fs -= tmp;
+    sec += tmp;
+    *seconds = sec;
+    *frac_seconds = fs;
+}
+
+void orc_fifo_destroy(orc_fifo *f) {
+    if (!f) return;
+    free(f->storage);
+    free(f);
+}

@@ -16,6 +16,7 @@
  */
 #ifndef SRCDSP_ORACLE_H
 #define SRCDSP_ORACLE_H
+#include <stddef.h>
 #include <stdint.h>
 #ifdef __cplusplus
 extern "C" {
@@ -82,6 +83,20 @@ void orc_corr_bit_samples(const orc_corr *c, int16_t *out_ci16);
 void orc_corr_status(const orc_corr *c, uint32_t *energy3, uint32_t *corr3, uint32_t *coeffs_energy,
                      int *coeff_scaling, double *threshold_factor);
 void orc_corr_destroy(orc_corr *c);
+
+/* ---- FifoWithTimeTrack<T, N> (buffers.h:58-459), element = elem_bytes ---- */
+typedef struct orc_fifo orc_fifo;
+orc_fifo *orc_fifo_create(size_t elem_bytes, size_t N, double sampling_frequency);
+/* returns -1 where the reference asserts (n >= N) */
+int orc_fifo_write(orc_fifo *f, const void *in, size_t n, unsigned seconds, double frac_seconds);
+/* returns 1 for the reference's `true` (range not available), 0 otherwise,
+ * -1 where the reference asserts (n == 0); *start may be raised to timeStart */
+int orc_fifo_read(orc_fifo *f, void *out, size_t n, uint64_t *start);
+size_t orc_fifo_count(const orc_fifo *f);
+void orc_fifo_reset(orc_fifo *f);
+void orc_fifo_absolute_time(const orc_fifo *f, uint64_t time_point, double frac_time_point, unsigned *seconds,
+                            double *frac_seconds);
+void orc_fifo_destroy(orc_fifo *f);
 
 /* ---- counter-based synthetic inputs shared by tests and bench ---- */
 uint64_t orc_splitmix64(uint64_t x);

@@ -66,6 +66,21 @@ SIGNATURES = {
     "srcdsp_corr_step_host": (I, [VP, VP, SZ, IP, IP]),
     "srcdsp_corr_get_bit_samples": (I, [VP, I16P]),
     "srcdsp_corr_get_status": (I, [VP, U32P, U32P, U32P, IP, DP]),
+    "srcdsp_fifo_create": (I, [HP, SZ, SZ, D]),
+    "srcdsp_fifo_destroy": (I, [VP]),
+    "srcdsp_fifo_write": (I, [VP, VP, SZ, U, D]),
+    "srcdsp_fifo_write_device": (I, [VP, VP, SZ, U, D, VP]),
+    "srcdsp_fifo_read": (I, [VP, VP, SZ, C.POINTER(C.c_uint64), IP, VP]),
+    "srcdsp_fifo_read_host": (I, [VP, VP, SZ, C.POINTER(C.c_uint64), IP]),
+    "srcdsp_fifo_count": (I, [VP, C.POINTER(C.c_size_t)]),
+    "srcdsp_fifo_reset": (I, [VP]),
+    "srcdsp_fifo_get_state": (I, [VP, C.POINTER(C.c_size_t), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), IP]),
+    "srcdsp_fifo_get_absolute_time": (I, [VP, U64, D, UP, DP]),
+    "srcdsp_iq_save": (I, [C.c_char_p, VP, SZ, SZ, I, VP]),
+    "srcdsp_iq_save_host": (I, [C.c_char_p, VP, SZ, SZ, I]),
+    "srcdsp_iq_count": (I, [C.c_char_p, SZ, C.POINTER(C.c_size_t)]),
+    "srcdsp_iq_load": (I, [C.c_char_p, SZ, VP, SZ, C.POINTER(C.c_size_t), VP]),
+    "srcdsp_iq_load_host": (I, [C.c_char_p, SZ, VP, SZ, C.POINTER(C.c_size_t)]),
     "srcdsp_last_error": (C.c_char_p, []),
     "srcdsp_version": (C.c_char_p, []),
     "srcdsp_fill_synthetic": (I, [VP, I, SZ, U64, U64, U64, I, I, VP]),

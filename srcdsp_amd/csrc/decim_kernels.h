@@ -384,7 +384,7 @@ __device__ __forceinline__ void store16(float4 *p, float4 v) {
     }
 }
 template <int NT, int R, int BLOCK, bool FMA, int MINW, bool Q0, int PROBE = 0, bool NTL = false, bool OST = false,
-          bool NTS = false, bool GS = false>
+          bool NTS = false, bool GS = false, bool PF2 = false>
 __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a) {
     constexpr int NQ = (NT + 3) / 4;
     constexpr int TO = BLOCK * R;
@@ -413,9 +413,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
     const long t_step = GS ? nb : kStep1;
     if (t_begin == 0 && t_end > 0) write_history(in, n_in, hist, (float2 *)a.hist_out[ch], H);
 
-    float4 v[PER];
+    float4 v[PER], v2[PER];
     // tiles >= 1: one descriptor per tile, 32-bit lane offsets, range-checked
-    auto stage_load = [&](long tile) {
+    auto stage_load = [&](float4 (&v)[PER], long tile) {
         if constexpr (PROBE == 2) tile = 1 + (tile & 15);
         const long b0 = 4 * tile * TO - 4 * NQ;  // >= 0 for tile >= 1
         const long remb = (n_in - b0) * 8;
@@ -444,11 +444,14 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
                 }
             }
         } else {
-            stage_load(t_begin);
+            stage_load(v, t_begin);
         }
+        if (PF2 && t_begin + t_step < t_end) stage_load(v2, t_begin + t_step);
     }
     const int Bt = 2 * NQ + KPAD + (PR + 1) * t;
-    for (long tile = t_begin; tile < t_end; tile += t_step) {
+    // PF2: two register sets alternate (tiles k and k+1 in flight while k is
+    // computed); otherwise one set, refilled right after it lands in LDS
+    auto do_tile = [&](long tile, float4 (&v)[PER]) {
         SRCDSP_LDS_BARRIER();
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
@@ -456,7 +459,11 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
             if (g < TG) lds[g + (g - 2 * NQ + KPAD * PR) / PR] = v[i];
         }
         SRCDSP_LDS_BARRIER();
-        if (tile + t_step < t_end) stage_load(tile + t_step);
+        if (PF2) {
+            if (tile + 2 * t_step < t_end) stage_load(v, tile + 2 * t_step);
+        } else if (tile + t_step < t_end) {
+            stage_load(v, tile + t_step);
+        }
 
         ConstPtr<float> tp = const_view<float>(a.coef);
         asm volatile("" : "+s"(tp));
@@ -528,7 +535,16 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
             for (int r = 0; r < R; ++r)
                 if (n0 + r < a.n_out) out[n0 + r] = make_float2(q(yr[r]), q(yi[r]));
         }
+        };
+    if constexpr (PF2) {
+        for (long tile = t_begin; tile < t_end; tile += 2 * t_step) {
+            do_tile(tile, v);
+            if (tile + t_step < t_end) do_tile(tile + t_step, v2);
+        }
+    } else {
+        for (long tile = t_begin; tile < t_end; tile += t_step) do_tile(tile, v);
     }
+
 }
 
 }  // namespace srcdsp

@@ -436,3 +436,67 @@ def fill_synthetic(t, kind: str, seed: int = 0x5EED, channel: int = 0, offset: i
     n = _nsamples(t, kind)
     A.call("srcdsp_fill_synthetic", _ptr(t), k, n, seed, channel, offset, lo, hi, _stream(t))
     return t
+
+
+# ================================================================ FIFO (8f.3)
+class FifoWithTimeTrack(_Handle):
+    """dsptl::FifoWithTimeTrack<T, N> (buffers.h:58-459) with its N-element
+    ring in HBM.  T is a numpy dtype (e.g. np.dtype(("<i2", 2)) for
+    complex<int16_t>, np.float64, np.complex64).  write() takes host (numpy,
+    staged through double-buffered pinned memory) or device (torch) input;
+    read() returns (error, start, out) -- the reference's bool, its start
+    after the call (raised to timeStart when it asked for older samples), and
+    the values (device tensor when `out` is one, else numpy)."""
+
+    _destroy = "srcdsp_fifo_destroy"
+
+    def __init__(self, dtype, N: int, samplingFrequency: float = 0.0):
+        self.dtype, self.N = np.dtype(dtype), int(N)
+        self._h = C.c_void_p()
+        A.call("srcdsp_fifo_create", C.byref(self._h), self.dtype.itemsize, self.N, float(samplingFrequency))
+
+    def _count_elems(self, x) -> int:
+        nb = x.numel() * x.element_size() if _is_device(x) else np.asarray(x).nbytes
+        if nb % self.dtype.itemsize:
+            raise ValueError("buffer is not a whole number of FIFO elements")
+        return nb // self.dtype.itemsize
+
+    def write(self, inp, seconds: int = 0, fracSeconds: float = 0.0):
+        n = self._count_elems(inp)
+        if _is_device(inp):
+            A.call("srcdsp_fifo_write_device", self._h, _ptr(inp), n, int(seconds), float(fracSeconds), _stream(inp))
+        else:
+            x = np.ascontiguousarray(inp)  # raw element bytes (a subarray dtype would broadcast)
+            A.call("srcdsp_fifo_write", self._h, C.c_void_p(x.ctypes.data), n, int(seconds), float(fracSeconds))
+
+    def read(self, out, start: int):
+        """out: an element count (host numpy result) or a buffer to fill."""
+        if isinstance(out, (int, np.integer)):
+            out = np.zeros(int(out), self.dtype)
+        n = self._count_elems(out)
+        st, err = C.c_uint64(int(start)), C.c_int(0)
+        if _is_device(out):
+            A.call("srcdsp_fifo_read", self._h, _ptr(out), n, C.byref(st), C.byref(err), _stream(out))
+        else:
+            A.call("srcdsp_fifo_read_host", self._h, C.c_void_p(out.ctypes.data), n, C.byref(st), C.byref(err))
+        return bool(err.value), st.value, out
+
+    def count(self) -> int:
+        c = C.c_size_t()
+        A.call("srcdsp_fifo_count", self._h, C.byref(c))
+        return c.value
+
+    def reset(self):
+        A.call("srcdsp_fifo_reset", self._h)
+
+    def state(self):
+        """(writePtr, timeStart, timeEnd, rolloverFlag) -- what dumpInfo() prints."""
+        wp, ts, te, ro = C.c_size_t(), C.c_uint64(), C.c_uint64(), C.c_int()
+        A.call("srcdsp_fifo_get_state", self._h, C.byref(wp), C.byref(ts), C.byref(te), C.byref(ro))
+        return wp.value, ts.value, te.value, bool(ro.value)
+
+    def getAbsoluteTime(self, timePoint: int, fracTimePoint: float = 0.0):
+        s, fs = C.c_uint(), C.c_double()
+        A.call("srcdsp_fifo_get_absolute_time", self._h, int(timePoint), float(fracTimePoint), C.byref(s),
+               C.byref(fs))
+        return s.value, fs.value

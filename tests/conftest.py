@@ -22,3 +22,14 @@ def pytest_configure(config):
 def golden():
     from replay import load_golden
     return load_golden()
+
+
+@pytest.fixture(scope="session")
+def S():
+    """The product package with its HIP library loaded (GPU tests only)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import srcdsp_amd
+    srcdsp_amd.lib()
+    return srcdsp_amd
