@@ -12,8 +12,10 @@
 #include <map>
 #include <vector>
 
+#include "buffers.h"
 #include "correlators.h"
 #include "dnsampling_filters.h"
+#include "dsptl_files.h"
 #include "filters.h"
 #include "mixers.h"
 #include "upsampling_filters.h"
@@ -127,6 +129,56 @@ int main(int argc, char **argv) {
                                   st.coeffScaling};
         out.put(107, r);
         out.put(108, corr.getRefBitSamples());
+    }
+    // 6. FifoWithTimeTrack<double, 15>: the scenario of the reference's own
+    //    buffers_test.cpp (its reads and counts)
+    {
+        dsptl::FifoWithTimeTrack<double, 15> fifo;
+        std::vector<double> input, res;
+        double value = 0;
+        auto block = [&](size_t n) {
+            input.assign(n, 0.0);
+            for (auto &e : input) e = (value += 1);
+        };
+        for (int i = 0; i < 23; ++i) {
+            block(14);
+            fifo.write(input);
+        }
+        res.push_back((double)fifo.count());
+        for (size_t n : {10, 5, 7}) {
+            block(n);
+            fifo.write(input);
+            res.push_back((double)fifo.count());
+        }
+        fifo.reset();
+        res.push_back((double)fifo.count());
+        value = 0;
+        const size_t reads[3][2] = {{3, 4}, {15, 3}, {4, 6}};
+        const size_t adds[3] = {7, 10, 4};
+        for (int k = 0; k < 3; ++k) {
+            block(adds[k]);
+            fifo.write(input);
+            std::vector<double> o(reads[k][0]);
+            uint64_t start = reads[k][1];
+            bool err = fifo.read(o, start);
+            res.push_back(err ? 1.0 : 0.0);
+            res.push_back((double)start);
+            res.insert(res.end(), o.begin(), o.end());
+        }
+        res.push_back((double)fifo.count());
+        out.put(109, res);
+    }
+    // 7. binary I/Q capture round trip through the drop-in dsptl_files.h
+    {
+        auto x = as<ci16>(in[3]);
+        {
+            std::ofstream os(argv[2] + std::string(".iq"), std::ios::binary);
+            dsptl::saveBinarySamples(x, os);
+        }
+        std::ifstream is(argv[2] + std::string(".iq"), std::ios::binary);
+        std::vector<ci16> back(5, ci16(1, 1));  // replaced, not appended to
+        dsptl::readBinarySamples(is, back);
+        out.put(110, back);
     }
     std::printf("dropin_main: ok\n");
     return 0;

@@ -35,7 +35,14 @@ def test_dropin_headers_compile_all_supported_instantiations(tmp_path):
 #include "upsampling_filters.h"
 #include "mixers.h"
 #include "correlators.h"
+#include "buffers.h"
+#include "dsptl_files.h"
 using cf32 = std::complex<float>; using ci16 = std::complex<int16_t>; using ci32 = std::complex<int32_t>;
+template class dsptl::FifoWithTimeTrack<ci16, 1 << 20>;
+template class dsptl::FifoWithTimeTrack<double, 15>;
+template void dsptl::saveBinarySamples<int16_t>(std::vector<ci16> &, std::ofstream &);
+template void dsptl::readBinarySamples<float>(std::ifstream &, std::vector<cf32> &);
+template size_t dsptl::readBinarySamples<int16_t>(const char *, dsptl::DeviceSpan<ci16>, void *);
 template class dsptl::FilterDnsamplingFir<cf32, cf32, cf32, float, 4>;
 template class dsptl::FilterDnsamplingFir<ci16, ci16, ci32, int32_t, 4>;
 template class dsptl::FilterDnsamplingFir<ci16, ci16, ci32, int16_t, 2>;
@@ -140,3 +147,16 @@ def test_dropin_program_matches_oracle(tmp_path):
     assert list(res[2:]) == [np.int32(np.uint32(st["corr"][0])), np.int32(np.uint32(st["energy"][0])),
                              st["coeff_scaling"]]
     assert got[108] == corr.bit_samples().tobytes()
+    # FIFO: the reference's buffers_test.cpp scenario vs the golden recorded from the reference
+    from io_replay import load
+    man, arr = load()
+    bt = next(c for c in man["fifo"] if c["name"] == "fifo_buffers_test")
+    exp = []
+    for op in bt["ops"]:
+        if op[0] == "count":
+            exp.append(float(op[1]))
+        elif op[0] == "read":
+            exp += [float(op[3]), float(op[4])] + list(arr[op[5]].astype(np.float64))
+    assert np.array_equal(np.frombuffer(got[109], np.float64), np.array(exp))
+    # I/Q: whole samples only, output replaced
+    assert got[110] == xi.tobytes()
