@@ -53,6 +53,13 @@ def parse():
     return p.parse_args()
 
 
+# "nccl" (= RCCL over xGMI) on a multi-GPU node.  SRCDSP_BENCH_BACKEND=gloo is
+# only for rehearsing the N > 1 code path with several ranks on ONE GPU (the
+# collectives then move host copies); its timings are not scaling numbers.
+BACKEND = os.environ.get("SRCDSP_BENCH_BACKEND", "nccl")
+COLL_DEV = "cuda" if BACKEND == "nccl" else None
+
+
 def dist_setup(args):
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -60,8 +67,12 @@ def dist_setup(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if BACKEND == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.cuda.set_device(local % torch.cuda.device_count())
+            dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
     return world, rank, local
@@ -162,7 +173,7 @@ class CorrWorkload(Workload):
         # clears the registers and history, then one step() scans to the hit
         self.g.reset()
         local = self.D.corr_segment_search(self.g, self.halo, self.x, self.s0)
-        first = self.D.first_detection(local, self.world, device="cuda")
+        first = self.D.first_detection(local, self.world, device=COLL_DEV)
         found = first != self.D.NO_DETECTION
         self.last = (found, first if found else -1)
 
@@ -339,7 +350,7 @@ def main():
         ev[i][1].record(stream)
     barrier(world)
     t1 = time.perf_counter()
-    wall = max_over_ranks(t1 - t0, world, device="cuda")
+    wall = max_over_ranks(t1 - t0, world, device=COLL_DEV)
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     kern_avg_ms = float(np.mean(kern_ms))
 
@@ -355,7 +366,7 @@ def main():
         # configs[2]: gather every rank's decimated channels to rank 0 over RCCL (xGMI)
         barrier(world)
         g0 = time.perf_counter()
-        bufs = gather_to_root(work.y, world, rank)
+        bufs = gather_to_root(work.y if COLL_DEV else work.y.cpu(), world, rank)
         barrier(world)
         gather_ms = (time.perf_counter() - g0) * 1e3
         del bufs

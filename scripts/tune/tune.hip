@@ -140,6 +140,8 @@ extern "C" int tune_decim(int variant, int grid, const float *d_coef, const void
     case 45: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 3, true, 0, true, true, true, true, true>, grid, 256, L, s);
     case 46: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 0, true, true, true, true, true>, grid, 256, L, s);
     case 47: L.ntiles = tiles(128 * 4); return launch(decim_stream2_cf32<127, 4, 128, true, 6, true, 0, true, true, true, true, true>, grid, 128, L, s);
+    case 48: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true>, grid, 512, L, s);
+    case 49: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 3, true, 0, true, true, true, true>, grid, 512, L, s);
     case 24: L.ntiles = tiles(128 * 8); return launch(decim_stream2_cf32<127, 8, 128, true, 2, true>, grid, 128, L, s);
     default: return -1;
     }

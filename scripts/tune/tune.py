@@ -74,9 +74,8 @@ def main():
             fn()
             med, mn = timeit(fn, 10)
             print(f"  {label}, {blocks} blocks: {mn:.4f} ms -> {bps * L / (mn * 1e-3) / 1e9:.1f} GB/s")
-    variants = [(42, 2048, "v2 GS ntl staged-nts g2048 (product)"), (45, 2048, "PF2 MINW3 g2048"),
-                (45, 1536, "PF2 MINW3 g1536"), (45, 768, "PF2 MINW3 g768"),
-                (47, 3072, "PF2 B128 MINW6 g3072"), (47, 1536, "PF2 B128 MINW6 g1536")]
+    variants = [(42, 2048, "product B256 g2048"), (48, 1024, "B512 g1024"), (48, 512, "B512 g512"),
+                (48, 2048, "B512 g2048"), (42, 1024, "product B256 g1024"), (42, 4096, "product B256 g4096")]
     if os.environ.get("TUNE_SUSTAINED_ONLY"):
         sustained_rounds(variants, x, y, cdev, h0, h1, stream, L, ref)
         return
