@@ -142,6 +142,9 @@ extern "C" int tune_decim(int variant, int grid, const float *d_coef, const void
     case 47: L.ntiles = tiles(128 * 4); return launch(decim_stream2_cf32<127, 4, 128, true, 6, true, 0, true, true, true, true, true>, grid, 128, L, s);
     case 48: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true>, grid, 512, L, s);
     case 49: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 3, true, 0, true, true, true, true>, grid, 512, L, s);
+    case 50: L.ntiles = tiles(1024 * 4); return launch(decim_stream2_cf32<127, 4, 1024, true, 4, true, 0, true, true, true, true>, grid, 1024, L, s);
+    case 51: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, false>, grid, 512, L, s);
+    case 52: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, false, true, true, true>, grid, 512, L, s);
     case 24: L.ntiles = tiles(128 * 8); return launch(decim_stream2_cf32<127, 8, 128, true, 2, true>, grid, 128, L, s);
     default: return -1;
     }

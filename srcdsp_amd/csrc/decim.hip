@@ -43,34 +43,36 @@ unsigned phase_step_tile(unsigned long N, unsigned long fr) {
     return (unsigned)(((4ul * kCiBlock_ * kCiR_) % N) * fr % N);
 }
 namespace {
-// cf32 tiles: 4 outputs per lane, 256 lanes -> 4096 input samples per tile,
-// 38 KB LDS and 124 VGPRs = 4 resident workgroups (16 waves) per CU; the
+// cf32 tiles: 4 outputs per lane, 512 lanes -> 8192 input samples per tile,
+// 75 KB LDS and 128 VGPRs = 2 resident workgroups (16 waves) per CU; the
 // persistent grid is 2x the resident capacity (measured best on MI355X:
 // scripts/tune, profiles/).
-constexpr int kCfR = 4, kCfBlock = 256, kCfGridCap = 2048;
+constexpr int kCfR = 4, kCfBlock = 512, kCfGrid = 1024;
+constexpr int kCfGridCap = 2048;  // persistent grid of the other streaming kernels
 constexpr int kCiR = 4, kCiBlock = 256;
 
 template <int NT>
 int launch_cf32(DecimLaunch L, int channels, bool fma, hipStream_t s) {
     constexpr int TO = kCfBlock * kCfR;
     L.ntiles = (L.n_out + TO - 1) / TO;
-    dim3 grid((unsigned)std::min<long>(L.ntiles, kCfGridCap), channels);
+    dim3 grid((unsigned)std::min<long>(L.ntiles, kCfGrid), channels);
     const bool q0 = (L.shift & 31u) == 0;  // limitScale16 shift 0: the 4-op float quantiser
-    // measured best (scripts/tune, sustained back-to-back): grid-stride tile
-    // order (GS), non-temporal input loads, outputs staged through LDS into
-    // whole-line non-temporal stores -- 5.7 % over contiguous runs / plain ops
+    // measured best (scripts/tune, sustained back-to-back): 512-lane tiles
+    // (8192 samples: half the halo re-read of 256), grid-stride tile order,
+    // non-temporal input loads, outputs staged through LDS into whole-line
+    // non-temporal stores; 2 workgroups (16 waves) per CU
+#define SRCDSP_CF32(F, Q) \
+    hipLaunchKernelGGL((decim_stream2_cf32<NT, kCfR, kCfBlock, F, 4, Q, 0, true, true, true, true>), grid, \
+                       dim3(kCfBlock), 0, s, L)
     if (fma && q0)
-        hipLaunchKernelGGL((decim_stream2_cf32<NT, kCfR, kCfBlock, true, 4, true, 0, true, true, true, true>), grid,
-                           dim3(kCfBlock), 0, s, L);
+        SRCDSP_CF32(true, true);
     else if (fma)
-        hipLaunchKernelGGL((decim_stream2_cf32<NT, kCfR, kCfBlock, true, 4, false, 0, true, true, true, true>), grid,
-                           dim3(kCfBlock), 0, s, L);
+        SRCDSP_CF32(true, false);
     else if (q0)
-        hipLaunchKernelGGL((decim_stream2_cf32<NT, kCfR, kCfBlock, false, 3, true, 0, true, true, true, true>), grid,
-                           dim3(kCfBlock), 0, s, L);
+        SRCDSP_CF32(false, true);
     else
-        hipLaunchKernelGGL((decim_stream2_cf32<NT, kCfR, kCfBlock, false, 3, false, 0, true, true, true, true>), grid,
-                           dim3(kCfBlock), 0, s, L);
+        SRCDSP_CF32(false, false);
+#undef SRCDSP_CF32
     return SRCDSP_OK;
 }
 
@@ -99,14 +101,22 @@ int launch_ci16_dot2(DecimLaunch L, int channels, bool mixed, hipStream_t s) {
 }
 
 template <int KV>
-int launch_fir_tile(const DecimLaunch &L, int channels, bool fma, hipStream_t s) {
+int launch_fir_tile(const DecimLaunch &L0, int channels, bool fma, hipStream_t s) {
     constexpr int TO = kFirR * kFirBlock;
     constexpr int SPG = FirTraits<KV>::SPG;
-    const int NQ = (L.ntaps + 3) / 4;
-    const int P0 = 8 * ((NQ + 1) / 2);
-    const int span = TO + P0;
+    DecimLaunch L = L0;
+    L.ntiles = (L.n_out + TO - 1) / TO;
+    if (L.ntaps <= kFirStreamTaps) {  // persistent, prefetching
+        dim3 grid((unsigned)std::min<long>(L.ntiles, kCfGridCap), channels);
+        if (fma)
+            hipLaunchKernelGGL((fir_stream_f32<KV, true>), grid, dim3(kFirBlock), 0, s, L);
+        else
+            hipLaunchKernelGGL((fir_stream_f32<KV, false>), grid, dim3(kFirBlock), 0, s, L);
+        return SRCDSP_OK;
+    }
+    const int span = TO + fir_halo(L.ntaps);
     const size_t smem = 16 * (size_t)(span / SPG + span / SPG / (kFirR / SPG) + 1);
-    dim3 grid((unsigned)((L.n_out + TO - 1) / TO), channels);
+    dim3 grid((unsigned)L.ntiles, channels);
     if (fma)
         hipLaunchKernelGGL((fir_tile_f32<KV, true>), grid, dim3(kFirBlock), smem, s, L);
     else

@@ -990,44 +990,16 @@ __device__ __forceinline__ float fir_mac(bool fma, float c, float x, float y) {
     return fma ? __builtin_fmaf(c, x, y) : y + c * x;
 }
 
+// The FIR arithmetic of one lane: R outputs from the staged LDS image `fl`
+// (lane base granule gb), N taps (runtime) through the constant view tp.
 template <int KV, bool FMA>
-__global__ __launch_bounds__(kFirBlock) void fir_tile_f32(DecimLaunch a) {
+__device__ __forceinline__ void fir_lane(const float4 *fl, int gb, int N, ConstPtr<float> tp, unsigned sh,
+                                         float2 (&o)[kFirR]) {
     typedef typename FirTraits<KV>::S S;
     constexpr int SPG = FirTraits<KV>::SPG;
-    constexpr int R = kFirR, BLOCK = kFirBlock, TO = R * BLOCK;
-    constexpr int GPL = R / SPG;  // granules per lane chunk
-    extern __shared__ float4 fl[];
-    const int N = a.ntaps, H = N - 1;
+    constexpr int R = kFirR, GPL = R / SPG;
     const int NQ = (N + 3) / 4;
-    const int P0 = 8 * ((NQ + 1) / 2);  // >= 4*NQ: the last chunk's window block
-    const int ch = blockIdx.y;
-    const S *in = (const S *)a.in + ch * a.in_stride;
-    const S *hist = (const S *)a.hist_in[ch];
-    float2 *out = (float2 *)a.out + ch * a.out_stride;
-    const long n_in = a.n_in;
-    const int t = threadIdx.x;
-    if (blockIdx.x == 0) write_history(in, n_in, hist, (S *)a.hist_out[ch], H);
-    const long o0 = (long)blockIdx.x * TO;  // first output (= input sample) of the tile
-    const int span = TO + P0;                // staged samples, origin o0 - P0
     auto slot = [&](int g) { return g + g / GPL; };
-    // stage: granule-wise, through the cache (halo from history on tile 0)
-    for (int g = t; g < span / SPG; g += BLOCK) {
-        const long s0 = o0 - P0 + (long)g * SPG;
-        float4 v;
-        if (s0 >= 0 && s0 + SPG <= n_in) {
-            v = *(const float4 *)(in + s0);
-        } else {
-            S w[SPG];
-#pragma unroll
-            for (int j = 0; j < SPG; ++j) w[j] = fetch(in, hist, s0 + j, n_in, H);
-            v = *(const float4 *)w;
-        }
-        fl[slot(g)] = v;
-    }
-    __syncthreads();
-    // lane base sample b = P0 + R*t; window sample m (relative to b) lives in
-    // granule (b + m) / SPG at slot(...)
-    const int gb = (P0 + R * t) / SPG;
     float yr[R];
     f2_t y2[R];
 #pragma unroll
@@ -1046,7 +1018,6 @@ __global__ __launch_bounds__(kFirBlock) void fir_tile_f32(DecimLaunch a) {
             dst[2] = make_float2(v1.x, v1.y); dst[3] = make_float2(v1.z, v1.w);
         }
     };
-    ConstPtr<float> tp = const_view<float>(a.coef);
     // chunk q: window blocks (lo = samples -4q-4.., mid = -4q.., hi = -4q+4..)
     auto chunk = [&](int q, const S (&lo)[4], const S (&mid)[4], const S (&hi)[4], bool guard) {
 #pragma unroll
@@ -1088,18 +1059,153 @@ __global__ __launch_bounds__(kFirBlock) void fir_tile_f32(DecimLaunch a) {
             chunk(q + 1, C, A, B, true);
         }
     }
-    const unsigned sh = a.shift;
-    const long n0 = o0 + (long)t * R;
-    float2 o[R];
 #pragma unroll
     for (int r = 0; r < R; ++r)
         o[r] = SPG == 4 ? make_float2(q16f(yr[r], sh), 0.f) : make_float2(q16f(y2[r].x, sh), q16f(y2[r].y, sh));
+}
+
+__host__ __device__ constexpr int fir_halo(int ntaps) { return 8 * (((ntaps + 3) / 4 + 1) / 2); }
+
+// one tile per workgroup, any tap count up to kFirMaxTaps (dynamic LDS)
+template <int KV, bool FMA>
+__global__ __launch_bounds__(kFirBlock) void fir_tile_f32(DecimLaunch a) {
+    typedef typename FirTraits<KV>::S S;
+    constexpr int SPG = FirTraits<KV>::SPG;
+    constexpr int R = kFirR, BLOCK = kFirBlock, TO = R * BLOCK;
+    constexpr int GPL = R / SPG;  // granules per lane chunk
+    extern __shared__ float4 fl[];
+    const int N = a.ntaps, H = N - 1;
+    const int P0 = fir_halo(N);  // >= 4*NQ: the last chunk's window block
+    const int ch = blockIdx.y;
+    const S *in = (const S *)a.in + ch * a.in_stride;
+    const S *hist = (const S *)a.hist_in[ch];
+    float2 *out = (float2 *)a.out + ch * a.out_stride;
+    const long n_in = a.n_in;
+    const int t = threadIdx.x;
+    if (blockIdx.x == 0) write_history(in, n_in, hist, (S *)a.hist_out[ch], H);
+    const long o0 = (long)blockIdx.x * TO;  // first output (= input sample) of the tile
+    const int span = TO + P0;                // staged samples, origin o0 - P0
+    auto slot = [&](int g) { return g + g / GPL; };
+    // stage: granule-wise, through the cache (halo from history on tile 0)
+    for (int g = t; g < span / SPG; g += BLOCK) {
+        const long s0 = o0 - P0 + (long)g * SPG;
+        float4 v;
+        if (s0 >= 0 && s0 + SPG <= n_in) {
+            v = *(const float4 *)(in + s0);
+        } else {
+            S w[SPG];
+#pragma unroll
+            for (int j = 0; j < SPG; ++j) w[j] = fetch(in, hist, s0 + j, n_in, H);
+            v = *(const float4 *)w;
+        }
+        fl[slot(g)] = v;
+    }
+    __syncthreads();
+    float2 o[R];
+    fir_lane<KV, FMA>(fl, (P0 + R * t) / SPG, N, const_view<float>(a.coef), a.shift, o);
+    const long n0 = o0 + (long)t * R;
     if (n0 + R <= a.n_out) {
 #pragma unroll
         for (int r = 0; r < R; r += 2) *(float4 *)(out + n0 + r) = make_float4(o[r].x, o[r].y, o[r + 1].x, o[r + 1].y);
     } else {
         for (int r = 0; r < R; ++r)
             if (n0 + r < a.n_out) out[n0 + r] = o[r];
+    }
+}
+
+// Persistent variant for <= kFirStreamTaps taps (the headline decimator's
+// memory schedule): grid-stride tile order, the next tile's buffer loads
+// (non-temporal, range-checked zero fill past the end) issued into VGPRs
+// right after this tile lands in LDS, outputs staged back through LDS into
+// whole-line non-temporal stores.
+constexpr int kFirStreamTaps = 128;
+
+template <int KV, bool FMA>
+__global__ __launch_bounds__(kFirBlock, 4) void fir_stream_f32(DecimLaunch a) {
+    typedef typename FirTraits<KV>::S S;
+    constexpr int SPG = FirTraits<KV>::SPG;
+    constexpr int R = kFirR, BLOCK = kFirBlock, TO = R * BLOCK;
+    constexpr int GPL = R / SPG;
+    constexpr int P0MAX = fir_halo(kFirStreamTaps);
+    constexpr int TGMAX = (TO + P0MAX) / SPG;  // staged granules, worst case
+    constexpr int PER = ceildiv(TGMAX, BLOCK);
+    constexpr int LSTAGE = TGMAX + TGMAX / GPL + 1;
+    constexpr int LOUT = TO * 8 / 16;          // output tile as float4
+    __shared__ float4 fl[LSTAGE > LOUT ? LSTAGE : LOUT];
+    const int N = a.ntaps, H = N - 1;
+    const int P0 = fir_halo(N);
+    const int TG = (TO + P0) / SPG;
+    const int ch = blockIdx.y;
+    const S *in = (const S *)a.in + ch * a.in_stride;
+    const S *hist = (const S *)a.hist_in[ch];
+    float2 *out = (float2 *)a.out + ch * a.out_stride;
+    const long n_in = a.n_in;
+    const int t = threadIdx.x;
+    const long nb = gridDim.x;
+    const long b = xcd_tile(blockIdx.x, nb);
+    if (b == 0) write_history(in, n_in, hist, (S *)a.hist_out[ch], H);
+    auto slot = [&](int g) { return g + g / GPL; };
+    float4 v[PER];
+    auto stage_load = [&](long tile) {  // tile >= 1 (its halo is input, not history)
+        const long s0 = tile * TO - P0;
+        const long remb = (n_in - s0) * (long)sizeof(S);
+        const unsigned nrec = (unsigned)(remb > 0xfffffff0L ? 0xfffffff0L : (remb < 0 ? 0 : remb));
+        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)(in + s0), 0, nrec, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int g = t + i * BLOCK;
+            if (g < TG) {
+                auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * g, 0, 2);  // aux 2 = nt
+                v[i] = make_float4(__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]),
+                                   __uint_as_float(w[3]));
+            }
+        }
+    };
+    if (b < a.ntiles) {
+        if (b == 0) {
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int g = t + i * BLOCK;
+                if (g < TG) {
+                    const long s0 = -P0 + (long)g * SPG;
+                    S w[SPG];
+#pragma unroll
+                    for (int j = 0; j < SPG; ++j) w[j] = fetch(in, hist, s0 + j, n_in, H);
+                    v[i] = *(const float4 *)w;
+                }
+            }
+        } else {
+            stage_load(b);
+        }
+    }
+    ConstPtr<float> tp = const_view<float>(a.coef);
+    for (long tile = b; tile < a.ntiles; tile += nb) {
+        SRCDSP_LDS_BARRIER();
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int g = t + i * BLOCK;
+            if (g < TG) fl[slot(g)] = v[i];
+        }
+        SRCDSP_LDS_BARRIER();
+        if (tile + nb < a.ntiles) stage_load(tile + nb);
+        float2 o[R];
+        fir_lane<KV, FMA>(fl, (P0 + R * t) / SPG, N, tp, a.shift, o);
+        const long o0 = tile * TO;
+        SRCDSP_LDS_BARRIER();  // every wave is done reading the staged input
+        float2 *ob = (float2 *)fl;
+#pragma unroll
+        for (int r = 0; r < R; ++r) ob[t * R + r] = o[r];
+        SRCDSP_LDS_BARRIER();
+        if (o0 + TO <= a.n_out) {
+#pragma unroll
+            for (int i = 0; i < LOUT / BLOCK; ++i) {
+                const int k = t + i * BLOCK;
+                store16<true>((float4 *)(out + o0) + k, fl[k]);
+            }
+        } else {
+            for (int k = t; k < TO; k += BLOCK)
+                if (o0 + k < a.n_out) out[o0 + k] = ob[k];
+        }
     }
 }
 
