@@ -49,6 +49,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=1 << 27, help="samples timed on the reference CPU path")
     p.add_argument("--no-gather", action="store_true")
+    p.add_argument("--dump-steps", action="store_true", help="print every timed step's kernel ms to stderr")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return p.parse_args()
 
@@ -353,6 +354,8 @@ def main():
     wall = max_over_ranks(t1 - t0, world, device=COLL_DEV)
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     kern_avg_ms = float(np.mean(kern_ms))
+    if args.dump_steps and rank == 0:
+        print("step_ms " + " ".join(f"{v:.4f}" for v in kern_ms), file=sys.stderr, flush=True)
 
     units_per_rank = L * (args.channels_per_gpu if args.workload == "decim" else 1) * args.steps
     if args.workload == "up":

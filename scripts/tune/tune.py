@@ -74,9 +74,7 @@ def main():
             fn()
             med, mn = timeit(fn, 10)
             print(f"  {label}, {blocks} blocks: {mn:.4f} ms -> {bps * L / (mn * 1e-3) / 1e9:.1f} GB/s")
-    variants = [(42, 2048, "product B256 g2048"), (48, 1024, "B512 g1024"), (48, 1536, "B512 g1536"),
-                (50, 256, "B1024 g256"), (50, 512, "B1024 g512"), (50, 768, "B1024 g768"),
-                (51, 1024, "B512 contig g1024"), (52, 1024, "B512 GS no-ntl g1024")]
+    variants = [(48, 1024, "B512 g1024 (product)"), (42, 2048, "B256 g2048 (previous)")]
     if os.environ.get("TUNE_SUSTAINED_ONLY"):
         sustained_rounds(variants, x, y, cdev, h0, h1, stream, L, ref)
         return

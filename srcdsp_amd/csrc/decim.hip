@@ -26,6 +26,7 @@
 // workgroup that owns tile 0 into the other ping-pong buffer, so a step is one
 // launch.
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "ops.h"
@@ -38,9 +39,9 @@ namespace srcdsp {
 namespace {
 constexpr int kCiR_ = 4, kCiBlock_ = 256;
 }
-// phase advance of the fused mixer per ci16 tile (4 * TO samples)
-unsigned phase_step_tile(unsigned long N, unsigned long fr) {
-    return (unsigned)(((4ul * kCiBlock_ * kCiR_) % N) * fr % N);
+// phase advance of the fused mixer per ci16 tile of `to` outputs (4*to samples)
+unsigned phase_step_tile(unsigned long N, unsigned long fr, unsigned long to) {
+    return (unsigned)(((4ul * to) % N) * fr % N);
 }
 namespace {
 // cf32 tiles: 4 outputs per lane, 512 lanes -> 8192 input samples per tile,
@@ -88,16 +89,38 @@ int launch_ci16(DecimLaunch L, int channels, bool mixed, hipStream_t s) {
     return SRCDSP_OK;
 }
 
+// dot2 ci16 kernel shape: tile lanes and mixer table form.  SRCDSP_CI16_VARIANT
+// (tuning only) selects 0: 256 lanes, 1: 512 lanes, 2: 256 lanes + doubled
+// table, 3: 512 lanes + doubled table.
+static int ci16_variant() {
+    static const int v = [] {
+        const char *e = std::getenv("SRCDSP_CI16_VARIANT");
+        return e ? std::atoi(e) : 3;
+    }();
+    return v;
+}
+
+template <int NT, int BLOCK, bool TAB2>
+int launch_ci16_dot2_shape(DecimLaunch L, int channels, bool mixed, hipStream_t s) {
+    constexpr int TO = BLOCK * kCiR;
+    L.ntiles = (L.n_out + TO - 1) / TO;
+    if (mixed) L.mix_dtile = phase_step_tile(L.mix_N, L.mix_freq, TO);
+    dim3 grid((unsigned)std::min<long>(L.ntiles, kCfGridCap * 256 / BLOCK), channels);
+    if (mixed)
+        hipLaunchKernelGGL((decim_dot2_ci16<NT, BLOCK, true, 4, TAB2>), grid, dim3(BLOCK), 0, s, L);
+    else
+        hipLaunchKernelGGL((decim_dot2_ci16<NT, BLOCK, false, 4>), grid, dim3(BLOCK), 0, s, L);
+    return SRCDSP_OK;
+}
+
 template <int NT>
 int launch_ci16_dot2(DecimLaunch L, int channels, bool mixed, hipStream_t s) {
-    constexpr int TO = kCiBlock * kCiR;  // = 4 * 256: phase_step_tile assumes this tile
-    L.ntiles = (L.n_out + TO - 1) / TO;
-    dim3 grid((unsigned)std::min<long>(L.ntiles, kCfGridCap), channels);
-    if (mixed)
-        hipLaunchKernelGGL((decim_dot2_ci16<NT, kCiBlock, true, 4>), grid, dim3(kCiBlock), 0, s, L);
-    else
-        hipLaunchKernelGGL((decim_dot2_ci16<NT, kCiBlock, false, 4>), grid, dim3(kCiBlock), 0, s, L);
-    return SRCDSP_OK;
+    switch (ci16_variant()) {
+    case 0: return launch_ci16_dot2_shape<NT, 256, false>(L, channels, mixed, s);
+    case 1: return launch_ci16_dot2_shape<NT, 512, false>(L, channels, mixed, s);
+    case 2: return launch_ci16_dot2_shape<NT, 256, true>(L, channels, mixed, s);
+    default: return launch_ci16_dot2_shape<NT, 512, true>(L, channels, mixed, s);
+    }
 }
 
 template <int KV>
@@ -310,7 +333,7 @@ static int core_step(FirCore &f, const void *d_in, size_t n_in, void *d_out, siz
         L.mix_phase0 = (unsigned)phi0;
         L.mix_freq = (unsigned)fr;
         L.mix_phase_tile0 = phase(-4 * kNQ);
-        L.mix_dtile = phase_step_tile(N, fr);
+        L.mix_dtile = phase_step_tile(N, fr, (unsigned long)kCiBlock_ * kCiR_);  // reset per kernel tile
         L.mix_phase_hist = phase((long)n_in - (f.ntaps - 1));
     }
     rc = decim_launch(f, L, 1, s, mix != nullptr);

@@ -760,6 +760,22 @@ __device__ __forceinline__ uint32_t hi16_pair(uint32_t a, uint32_t b) {  // (hi 
 __device__ __forceinline__ int32_t sdot2(uint32_t a, uint32_t b, int32_t c) {
     return __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t_, a), __builtin_bit_cast(short2_t_, b), c, false);
 }
+// dot2 into a fresh accumulator: the VOP3 form with an inline 0 (the compiler
+// otherwise materialises the 0 with a v_mov for the accumulating VOP2 form)
+__device__ __forceinline__ int32_t sdot2_0(uint32_t a, uint32_t b) {
+    int32_t r;
+    asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// two mixer outputs (int32, >> 14 pending) -> one packed int16 pair clamped to
+// +-32767 (limitScale16; |v >> 14| < 2^17 so INT_MIN never occurs):
+// saturating v_cvt_pk_i16_i32, then v_pk_max_i16 with -32767
+__device__ __forceinline__ uint32_t clamp_pair_s14(int32_t a, int32_t b) {
+    const short2_t_ p = __builtin_amdgcn_cvt_pk_i16(a >> 14, b >> 14);
+    const short2_t_ lo = {-32767, -32767};
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(p, lo));
+}
+
 // mixers.h:169-188 on one packed sample with the (lr, li) table word
 __device__ __forceinline__ void mix_dot2(uint32_t w, uint32_t C, int32_t &re, int32_t &im) {
     const uint32_t A = __builtin_bit_cast(uint32_t, __builtin_bit_cast(short2_t_, C) * (short2_t_){1, -1});
@@ -768,7 +784,11 @@ __device__ __forceinline__ void mix_dot2(uint32_t w, uint32_t C, int32_t &re, in
     im = clamp_s14(sdot2(ws, C, 0));
 }
 
-template <int NT, int BLOCK, bool MIX, int MINW>
+// TAB2 (mixer): the (lr, li) table stored twice (2N words), so the address of
+// sample j of staged granule i is one add of a wave-uniform tile/granule
+// phase (SGPR) and a per-lane constant (4t + j)*freq mod N -- no per-sample
+// modulo; products via VOP3 dot2 and the pair clamp above.
+template <int NT, int BLOCK, bool MIX, int MINW, bool TAB2 = false>
 __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     constexpr int R = 4;
     constexpr int J = NT / 2 + 1;                 // tap pairs
@@ -779,7 +799,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     constexpr int PER = ceildiv(TG, BLOCK);
     constexpr int PG = (4 * TO + HS) / 8;         // plane granules
     constexpr int LSLOTS = 5 * ceildiv(PG, 2);
-    constexpr int TABMAX = MIX ? 4096 : 1;
+    constexpr int TABMAX = MIX ? (TAB2 ? 8192 : 4096) : 1;
     static_assert(HS % 16 == 0 && 2 * (J - 1) <= HS, "halo geometry");
     __shared__ uint4 lds[LSLOTS];
     __shared__ uint32_t ctab[TABMAX];
@@ -800,10 +820,11 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
 
     if constexpr (MIX) {
         const int16_t *tab = a.mix_table;
-        for (int i = t; i < (int)N; i += BLOCK) {
-            unsigned ic = i + N / 4;
+        for (int i = t; i < (TAB2 ? 2 : 1) * (int)N; i += BLOCK) {
+            const unsigned k = (unsigned)i < N ? (unsigned)i : (unsigned)i - N;
+            unsigned ic = k + N / 4;
             ic = ic >= N ? ic - N : ic;
-            ctab[i] = ((uint32_t)(uint16_t)tab[ic]) | ((uint32_t)(uint16_t)tab[i] << 16);
+            ctab[i] = ((uint32_t)(uint16_t)tab[ic]) | ((uint32_t)(uint16_t)tab[k] << 16);
         }
         __syncthreads();
     }
@@ -856,6 +877,26 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
         *lds_half(g, 1) = make_uint2(hi16_pair(w0, w1), hi16_pair(w2, w3));
     };
     // mixes the granule in place (MIX) and writes both planes
+    // TAB2: per-lane byte offsets of the 4 samples of a staged granule
+    unsigned lj[4] = {0, 0, 0, 0};
+    if constexpr (MIX && TAB2)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) lj[j] = 4u * phase_add(0, 4 * t + j);
+    auto put_mixed2 = [&](int g, uint4 w, unsigned sb) {  // sb: granule phase * 4 (uniform)
+        const uint32_t *tb = ctab;
+        auto ld = [&](int j) { return *(const uint32_t *)((const char *)tb + (sb + lj[j])); };
+        const uint32_t c0 = ld(0), c1 = ld(1), c2 = ld(2), c3 = ld(3);
+        auto neg_hi = [](uint32_t c) {
+            return __builtin_bit_cast(uint32_t, __builtin_bit_cast(short2_t_, c) * (short2_t_){1, -1});
+        };
+        auto swp = [](uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); };
+        const int32_t r0 = sdot2_0(w.x, neg_hi(c0)), i0 = sdot2_0(swp(w.x), c0);
+        const int32_t r1 = sdot2_0(w.y, neg_hi(c1)), i1 = sdot2_0(swp(w.y), c1);
+        const int32_t r2 = sdot2_0(w.z, neg_hi(c2)), i2 = sdot2_0(swp(w.z), c2);
+        const int32_t r3 = sdot2_0(w.w, neg_hi(c3)), i3 = sdot2_0(swp(w.w), c3);
+        *lds_half(g, 0) = make_uint2(clamp_pair_s14(r0, r1), clamp_pair_s14(r2, r3));
+        *lds_half(g, 1) = make_uint2(clamp_pair_s14(i0, i1), clamp_pair_s14(i2, i3));
+    };
     auto put_mixed = [&](int g, uint4 w, unsigned ph) {
         if constexpr (MIX) {
             int32_t r0, i0, r1, i1, r2, i2, r3, i3;
@@ -894,7 +935,15 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     const int lb = 2 * t + HG;  // lane's first plane granule
     for (long tile = t_begin; tile < t_end; ++tile) {
         SRCDSP_LDS_BARRIER();
-        if (MIX && tile != 0) {
+        if (MIX && TAB2 && tile != 0) {
+            unsigned sp = tile_phase(tile);  // wave-uniform
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int g = t + i * BLOCK;
+                if (g < TG) put_mixed2(g, v[i], 4u * sp);
+                sp = adv(sp, d_i);
+            }
+        } else if (MIX && tile != 0) {
             unsigned ph = adv(tile_phase(tile), d_lane);
 #pragma unroll
             for (int i = 0; i < PER; ++i) {
