@@ -40,8 +40,12 @@ SEED = 0x5EED
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    # The chip's clocks settle only after ~50 back-to-back launches (measured:
+    # steps 0-20 of a cold start average 0.65 ms for the headline, 0.49 ms from
+    # step 50 on -- profiles/r01_warmup_ramp_*.txt), so the default warm-up
+    # is 100 untimed steps before 200 timed ones (~0.15 s of GPU time).
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=100)
     p.add_argument("--workload", default="decim", choices=["decim", "mixdecim", "corr", "fir", "up"])
     p.add_argument("--samples", type=int, default=1 << 28, help="input samples per channel per step")
     p.add_argument("--channels-per-gpu", type=int, default=1)

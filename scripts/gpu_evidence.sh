@@ -24,15 +24,15 @@ for s in ${STEPS:-tests bench prof pmc}; do
     bench)
       step bench_decim_$TAG 300 python bench.py
       step bench_mixdecim_$TAG 300 python bench.py --workload mixdecim
-      step bench_corr_$TAG 300 python bench.py --workload corr --samples 67108864 --steps 3 --warmup 1
-      step bench_fir_$TAG 300 python bench.py --workload fir --steps 10
-      step bench_up_$TAG 300 python bench.py --workload up --steps 10 --no-cpu-baseline ;;
+      step bench_corr_$TAG 300 python bench.py --workload corr --samples 67108864
+      step bench_fir_$TAG 300 python bench.py --workload fir
+      step bench_up_$TAG 300 python bench.py --workload up --no-cpu-baseline ;;
     prof)
-      prof decim --steps 20 --warmup 3
-      prof mixdecim --steps 20 --warmup 3
-      prof corr --samples 67108864 --steps 3 --warmup 1
-      prof fir --steps 10 --warmup 2
-      prof up --steps 10 --warmup 2 ;;
+      prof decim
+      prof mixdecim
+      prof corr --samples 67108864 --steps 50 --warmup 20
+      prof fir
+      prof up ;;
     pmc)
       step pmc_decim_$TAG 600 python scripts/pmc_traffic.py --workload decim --tag $TAG
       step pmc_mixdecim_$TAG 600 python scripts/pmc_traffic.py --workload mixdecim --tag $TAG ;;
