@@ -241,6 +241,176 @@ __global__ __launch_bounds__(kCBlock) void corr_eval_s1(const uint32_t *__restri
     }
 }
 
+// ------------------------------------ S == 1: one launch, detection fused
+// corr_eval_s1's arithmetic over the whole call in ONE launch, with the
+// peak/threshold test of correlators.h:262-268 evaluated by each block on its
+// own 4096 outputs and reduced to the first hit with atomicMin(best).
+//  * the test at a block's first two outputs needs corr/energy of the two
+//    samples before it: wave 0 computes those two outputs itself (16 taps per
+//    lane from L2, wave reduction), or takes the previous call's registers at
+//    index 0;
+//  * a block whose first output lies past a recorded hit returns at once, and
+//    a running block re-reads `best` every 256 taps and stops computing once
+//    a hit before it is known -- the scan ends near the first detection, as
+//    the reference's `break` does, with no host round trip.
+__device__ __forceinline__ uint32_t corr_value(int32_t ar, int32_t ai, unsigned cs) {
+    const int32_t sr = ar >> (cs & 31u), si = ai >> (cs & 31u);  // scale32 :244
+    const int32_t qr = sr >> 2, qi = si >> 2;                    // :250
+    return (uint32_t)qr * (uint32_t)qr + (uint32_t)qi * (uint32_t)qi;
+}
+
+__device__ __forceinline__ unsigned load_best(const unsigned *best) {
+    return __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(kCBlock) void corr_scan_s1(const uint32_t *__restrict__ in, long n,
+                                                         const uint32_t *__restrict__ hist,
+                                                         const uint32_t *__restrict__ ptaps, int N, unsigned cs,
+                                                         uint32_t c_prev0, uint32_t c_prev1, uint32_t e_prev0,
+                                                         uint32_t *__restrict__ corr_out,
+                                                         uint32_t *__restrict__ en_out, unsigned *best) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t xs[];
+    __shared__ uint32_t prev_c[kCBlock + 1][2], prev_e[kCBlock + 1];
+    __shared__ unsigned dead_any, best0;
+    constexpr int TO = kCBlock * kCR;
+    const long i0 = (long)blockIdx.x * TO;  // first output of the tile
+    if (threadIdx.x == 0) best0 = load_best(best);
+    __syncthreads();
+    if ((long)best0 < i0) return;  // a hit before this tile is already known (block-uniform)
+    const long base = i0 - (N - 1);
+    const int span = TO + N - 1;
+    auto lw = [&](int l) { int lp = l + 1; return lp + 4 * (lp / kCR); };
+    for (int l = threadIdx.x; l < span; l += kCBlock) {
+        long j = base + l;
+        uint32_t w = 0;
+        if (j < n) w = j >= 0 ? in[j] : (j + (N - 1) >= 0 ? hist[j + (N - 1)] : 0u);
+        xs[lw(l)] = w;
+    }
+    if (threadIdx.x == 0) dead_any = 0;
+    __syncthreads();
+    const int t = threadIdx.x;
+    int32_t ar[kCR], ai[kCR];
+#pragma unroll
+    for (int r = 0; r < kCR; ++r) ar[r] = ai[r] = 0;
+    int32_t e0 = 0;
+    const int lb = t * kCR;
+    uint32_t A[kCR + 15], B[kCR + 15];
+#pragma unroll
+    for (int j = 0; j < kCR - 1; ++j) B[16 + j] = xs[lw(lb + j)];
+    ConstPtr<uint32_t> tp = const_view<uint32_t>(ptaps);
+    auto chunk = [&](int m0, uint32_t(&cur)[kCR + 15], const uint32_t(&prev)[kCR + 15]) {
+        asm volatile("" : "+s"(tp));
+        uint32_t pw[32];
+#pragma unroll
+        for (int k = 0; k < 32; ++k) pw[k] = tp[2 * m0 + k];
+        const uint4 *src = (const uint4 *)xs + 5 * (t + 1 + (m0 >> 4));
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const uint4 q = src[g];
+            cur[kCR - 1 + 4 * g + 0] = q.x;
+            cur[kCR - 1 + 4 * g + 1] = q.y;
+            cur[kCR - 1 + 4 * g + 2] = q.z;
+            cur[kCR - 1 + 4 * g + 3] = q.w;
+        }
+        auto word = [&](int j) { return j < kCR - 1 ? prev[16 + j] : cur[j]; };
+#pragma unroll
+        for (int mm = 0; mm < 16; ++mm) {
+            const uint32_t p0 = pw[2 * mm], p1 = pw[2 * mm + 1];
+            const short2_t x0 = __builtin_bit_cast(short2_t, word(mm));
+            e0 = __builtin_amdgcn_sdot2(x0, x0, e0, false);
+#pragma unroll
+            for (int r = 0; r < kCR; ++r) {
+                const short2_t x = __builtin_bit_cast(short2_t, word(mm + r));
+                ar[r] = __builtin_amdgcn_sdot2(x, __builtin_bit_cast(short2_t, p0), ar[r], false);
+                ai[r] = __builtin_amdgcn_sdot2(x, __builtin_bit_cast(short2_t, p1), ai[r], false);
+            }
+        }
+    };
+    bool dead = false;
+    int m0 = 0;
+    for (int it = 0; m0 + 32 <= N; m0 += 32, ++it) {
+        chunk(m0, A, B);
+        chunk(m0 + 16, B, A);
+        if ((it & 7) == 7) {  // every 256 taps: has a hit before this tile been found?
+            const unsigned bb = __builtin_amdgcn_readfirstlane(load_best(best));
+            if ((long)bb < i0) {
+                dead = true;
+                break;
+            }
+        }
+    }
+    if (!dead && m0 < N) chunk(m0, A, B);
+    // the two outputs before the tile (for the test at its first two indices)
+    if (t < 64) {
+        uint32_t ex_c[2] = {c_prev0, c_prev1}, ex_e = e_prev0;
+        if (i0 > 0 && !dead) {
+            int32_t r1 = 0, q1 = 0, r2 = 0, q2 = 0, en1 = 0;
+            for (int m = t; m < N; m += 64) {  // output i0-1-u: sample i0-1-u-(N-1)+m
+                const uint32_t xa = corr_fetch(in, hist, i0 - N + m, N - 1);      // u = 0
+                const uint32_t xb = corr_fetch(in, hist, i0 - N - 1 + m, N - 1);  // u = 1
+                const short2_t sa = __builtin_bit_cast(short2_t, xa), sb = __builtin_bit_cast(short2_t, xb);
+                const short2_t p0 = __builtin_bit_cast(short2_t, (uint32_t)tp[2 * m]);
+                const short2_t p1 = __builtin_bit_cast(short2_t, (uint32_t)tp[2 * m + 1]);
+                r1 = __builtin_amdgcn_sdot2(sa, p0, r1, false);
+                q1 = __builtin_amdgcn_sdot2(sa, p1, q1, false);
+                r2 = __builtin_amdgcn_sdot2(sb, p0, r2, false);
+                q2 = __builtin_amdgcn_sdot2(sb, p1, q2, false);
+                en1 = __builtin_amdgcn_sdot2(sa, sa, en1, false);
+            }
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) {
+                r1 += __shfl_xor(r1, off);
+                q1 += __shfl_xor(q1, off);
+                r2 += __shfl_xor(r2, off);
+                q2 += __shfl_xor(q2, off);
+                en1 += __shfl_xor(en1, off);
+            }
+            ex_c[0] = corr_value(r1, q1, cs);
+            ex_c[1] = corr_value(r2, q2, cs);
+            ex_e = (uint32_t)en1 >> ((unsigned)((int)cs / 2) & 31u);
+        }
+        if (t == 0) {
+            prev_c[0][0] = ex_c[0];
+            prev_c[0][1] = ex_c[1];
+            prev_e[0] = ex_e;
+        }
+    }
+    // this lane's correlation values and (sliding) energies
+    uint32_t cv[kCR], ev[kCR];
+    uint32_t e = (uint32_t)e0;
+#pragma unroll
+    for (int r = 0; r < kCR; ++r) {
+        if (r > 0) {  // E_i = E_{i-1} + |x_i|^2 - |x_{i-N}|^2
+            const uint32_t xn = xs[lw(lb + r + N - 1)], xo = xs[lw(lb + r - 1)];
+            const short2_t a = __builtin_bit_cast(short2_t, xn), b = __builtin_bit_cast(short2_t, xo);
+            e += (uint32_t)__builtin_amdgcn_sdot2(a, a, 0, false) - (uint32_t)__builtin_amdgcn_sdot2(b, b, 0, false);
+        }
+        cv[r] = corr_value(ar[r], ai[r], cs);
+        ev[r] = e >> ((unsigned)((int)cs / 2) & 31u);
+    }
+    prev_c[t + 1][0] = cv[kCR - 1];
+    prev_c[t + 1][1] = cv[kCR - 2];
+    prev_e[t + 1] = ev[kCR - 1];
+    if (dead) dead_any = 1;
+    __syncthreads();
+    if (dead_any) return;  // outputs past a known hit: nothing to record
+    const uint32_t cm1 = prev_c[t][0], cm2 = prev_c[t][1], em1 = prev_e[t];
+    long hit = -1;
+#pragma unroll
+    for (int r = 0; r < kCR; ++r) {
+        const long i = i0 + lb + r;
+        if (i < n) {
+            corr_out[i] = cv[r];
+            en_out[i] = ev[r];
+            const uint32_t c1 = r >= 1 ? cv[r - 1] : cm1;
+            const uint32_t c2 = r >= 2 ? cv[r - 2] : (r == 1 ? cm1 : cm2);
+            const uint32_t e1 = r >= 1 ? ev[r - 1] : em1;
+            if (hit < 0 && corr_hit(c2, c1, cv[r], e1)) hit = i;
+        }
+    }
+    if (hit >= 0) atomicMin(best, (unsigned)hit);
+}
+
 __global__ void corr_detect(const uint32_t *__restrict__ corr, const uint32_t *__restrict__ en, long i_begin,
                             long i_end, uint32_t c_prev0, uint32_t c_prev1, uint32_t e_prev0, unsigned *best) {
     // skip when an EARLIER segment detected (a hit of this segment is >= i_begin,
@@ -302,7 +472,17 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
     const unsigned none = 0xffffffffu;
     unsigned best = none;
     SRCDSP_HIP_TRY(hipMemsetAsync(c.d_best, 0xff, 4, s));
-    for (long sb = detect ? 0 : std::max(0L, n - 3); sb < n; sb += seg) {
+    if (fast && detect) {  // one launch, detection fused, in-flight early exit
+        constexpr long TO = (long)kCBlock * kCR;
+        const long blocks = (n + TO - 1) / TO;
+        const size_t smem = 4 * (size_t)(((TO + c.N + 1) / kCR + 2) * (kCR + 4));
+        hipLaunchKernelGGL(corr_scan_s1, dim3((unsigned)blocks), dim3(kCBlock), smem, s, d_in, n, hist, c.d_ptaps,
+                           (int)c.N, cs, c.corr[0], c.corr[1], c.energy[0], c.d_corr, c.d_en, c.d_best);
+        SRCDSP_HIP_TRY(hipGetLastError());
+    }
+    // the segmented path: priming (the last 3 positions only) and the generic
+    // kernels (S > 1 or N % 16 != 0)
+    for (long sb = detect ? (fast ? n : 0) : std::max(0L, n - 3); sb < n; sb += seg) {
         const long se = std::min(n, sb + seg);
         if (fast) {
             constexpr long TO = (long)kCBlock * kCR;
