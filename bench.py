@@ -229,7 +229,7 @@ def cpu_baseline(args):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     from srcdsp_amd.design import hamming_sinc
-    if args.workload in ("mixdecim", "corr"):
+    if args.workload in ("mixdecim", "corr", "fir", "up"):
         return cpu_baseline_other(args, pyoracle)
     if args.workload != "decim":
         return None
@@ -299,6 +299,22 @@ def cpu_baseline_other(args, pyoracle):
         d.step(m.step(x))
         secs = time.perf_counter() - t0
         what = "Mixer<ci16,ci16,int16_t,4096>::step then FilterDnsamplingFir<ci16,ci16,ci32,int32_t,4>::step"
+    elif args.workload == "fir":
+        n = min(1 << 25, args.samples)
+        x = np.random.default_rng(0).integers(-2048, 2048, n).astype(np.float32)
+        f = ref.fir(1, hamming_sinc(31, 0.2))
+        t0 = time.perf_counter()
+        f.step(x)
+        secs = time.perf_counter() - t0
+        what = "FilterFir<float,complex<float>,float,float>::step, 31 taps (config 1's operator)"
+    elif args.workload == "up":
+        n = min(1 << 21, args.samples // 4)
+        x = o.gen_ci16(SEED, 0, 0, n, -8192, 8191)
+        u = ref.up(0, 4, q14(hamming_sinc(128, 0.12) * 4))
+        t0 = time.perf_counter()
+        u.step(x)
+        secs = time.perf_counter() - t0
+        what = "FilterUpsamplingFir<ci16,ci16,ci32,int32_t,4>::step, 128 taps (input samples/s)"
     else:
         n = min(1 << 22, args.samples)
         p = qpsk_pattern(1024, 500, seed=2)

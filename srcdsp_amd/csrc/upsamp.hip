@@ -19,6 +19,7 @@
 namespace srcdsp {
 
 enum { UV_CI16_I32 = 0, UV_CI16_I16 = 1, UV_I16_I32 = 2 };
+typedef short short2_t_u __attribute__((ext_vector_type(2)));
 
 struct srcdsp_up_state {
     int variant = 0;
@@ -28,6 +29,8 @@ struct srcdsp_up_state {
     int left_shift_factor = 0;
     int32_t *d_coef = nullptr;  // polyphase order: d_coef[o*H + i] = c[o + i*L]
     bool coef_i24 = false;      // every tap in (-2^23, 2^23): v_mad_i32_i24
+    bool coef_i16 = false;      // every tap in int16 range: v_dot2 tap pairs (variant 0)
+    uint32_t *d_pair = nullptr; // per phase o: pairs[o*(H/2+1) + p] = (lo c_o[2p], hi c_o[2p-1])
     void *d_hist[2] = {nullptr, nullptr};
     size_t hist_cap = 0;
     int cur = 0;
@@ -202,6 +205,146 @@ __global__ __launch_bounds__(kUpBlock) void up_tile(const uint32_t *in, long n_i
     }
 }
 
+// Tiled polyphase interpolator on v_dot2_i32_i16 (variant 0 with int16-range
+// taps, LR in {2, 4}).  Each lane owns RD = 8 consecutive input samples.  Taps
+// of phase o are paired P_p = (lo c_o[2p], hi c_o[2p-1]); the pair of input j
+// reads the packed samples (x[j-2p], x[j-2p+1]), which for even j is dword
+// (j-2p)/2 of an even-aligned plane E[e] = (x[2e], x[2e+1]) and for odd j dword
+// (j-1-2p)/2 of an odd-aligned plane O[e] = (x[2e+1], x[2e+2]).  A lane's 8
+// inputs read E[4t'+r/2-p] / O[4t'+(r-1)/2-p]: one 4-dword register window per
+// plane and component sliding one dword per pair, one ds_read_b128 per plane
+// every 4 pairs.  int16 x int16 -> int32 products, wrap-around accumulate:
+// exactly the reference's complex<int32_t> arithmetic.
+constexpr int kUpRD = 8, kUpBlockD = 256;
+
+template <int LR>
+__global__ __launch_bounds__(kUpBlockD) void up_tile_dot2(const uint32_t *in, long n_in, long n_total,
+                                                         const uint32_t *hist_in, uint32_t *hist_out,
+                                                         const uint32_t *pairs, int H, unsigned shift, uint32_t *out) {
+    constexpr int R = kUpRD, TI = R * kUpBlockD;
+    extern __shared__ uint4 ug[];  // 4 planes (E_re, E_im, O_re, O_im) of PGR granules each
+    const int Hm1 = H - 1;
+    const int PP = H / 2 + 1;            // pairs per phase
+    const int HG = (PP + 3) / 4;         // halo granules per plane (window reach)
+    const int PGR = TI / 8 + HG;         // granules per plane (4 dwords = 8 samples)
+    const int t = threadIdx.x;
+    if (blockIdx.x == 0) {
+        for (int k = t; k < Hm1; k += kUpBlockD) {
+            const long j = n_total - Hm1 + k;
+            hist_out[k] = up_fetch<UV_CI16_I32>(in, hist_in, j, n_in, Hm1);
+        }
+    }
+    const long j0 = (long)blockIdx.x * TI;
+    // staging: sample granule g (4 samples from j0 - 8*HG + 4g) -> plane dwords 2g, 2g+1
+    uint32_t *pl = (uint32_t *)ug;
+    const int PDW = 4 * PGR;  // dwords per plane
+    const int ng = 2 * PGR;
+    for (int g = t; g < ng; g += kUpBlockD) {
+        const long s0 = j0 - 8L * HG + 4L * g;
+        uint32_t w[5];
+        if (s0 >= 0 && s0 + 5 <= n_in) {
+            const uint4 v = *(const uint4 *)(in + s0);
+            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+            w[4] = in[s0 + 4];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 5; ++k) w[k] = up_fetch<UV_CI16_I32>(in, hist_in, s0 + k, n_in, Hm1);
+        }
+        auto lo = [](uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x05040100u); };
+        auto hi = [](uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x07060302u); };
+        *(uint2 *)&pl[0 * PDW + 2 * g] = make_uint2(lo(w[0], w[1]), lo(w[2], w[3]));
+        *(uint2 *)&pl[1 * PDW + 2 * g] = make_uint2(hi(w[0], w[1]), hi(w[2], w[3]));
+        *(uint2 *)&pl[2 * PDW + 2 * g] = make_uint2(lo(w[1], w[2]), lo(w[3], w[4]));
+        *(uint2 *)&pl[3 * PDW + 2 * g] = make_uint2(hi(w[1], w[2]), hi(w[3], w[4]));
+    }
+    __syncthreads();
+    // lane base: input j0 + 8t = plane dword D0 = 4t + 4*HG (granule gb).  Input
+    // r, pair p reads dword D0 + k - p, k = r/2 (plane E for even r, O for odd):
+    // for the chunk of pairs 4q..4q+3 those are dwords of granules gb - q
+    // (`cur`) and gb - q - 1 (`nxt`), two register sets that swap roles.
+    const int gb = t + HG;
+    int32_t yr[LR][R], yi[LR][R];
+#pragma unroll
+    for (int o = 0; o < LR; ++o)
+#pragma unroll
+        for (int r = 0; r < R; ++r) yr[o][r] = yi[o][r] = 0;
+    ConstPtr<uint32_t> tp = const_view<uint32_t>(pairs);
+    uint32_t W0[4][4], W1[4][4];  // [plane][dword]
+    auto load = [&](uint32_t (&w)[4][4], int gi) {
+#pragma unroll
+        for (int pl4 = 0; pl4 < 4; ++pl4) {
+            const uint4 v = ug[pl4 * PGR + gi];
+            w[pl4][0] = v.x; w[pl4][1] = v.y; w[pl4][2] = v.z; w[pl4][3] = v.w;
+        }
+    };
+    auto chunk = [&](int q, const uint32_t (&cur)[4][4], uint32_t (&nxt)[4][4]) {
+        asm volatile("" : "+s"(tp));
+        load(nxt, gb - q - 1);
+#pragma unroll
+        for (int pp = 0; pp < 4; ++pp) {
+            const int p = 4 * q + pp;
+            if (p >= PP) break;
+            uint32_t P[LR];
+#pragma unroll
+            for (int o = 0; o < LR; ++o) P[o] = tp[o * PP + p];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int k = r >> 1, rel = k - pp;  // -3..3
+                const int pr = (r & 1) ? 2 : 0, pi = pr + 1;  // planes E_re/E_im or O_re/O_im
+                const uint32_t xr = rel >= 0 ? cur[pr][rel] : nxt[pr][rel + 4];
+                const uint32_t xi = rel >= 0 ? cur[pi][rel] : nxt[pi][rel + 4];
+#pragma unroll
+                for (int o = 0; o < LR; ++o) {
+                    yr[o][r] = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t_u, xr),
+                                                      __builtin_bit_cast(short2_t_u, P[o]), yr[o][r], false);
+                    yi[o][r] = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t_u, xi),
+                                                      __builtin_bit_cast(short2_t_u, P[o]), yi[o][r], false);
+                }
+            }
+        }
+    };
+    load(W0, gb);
+    const int NQ = (PP + 3) / 4;
+    int q = 0;
+    for (; q + 2 <= NQ; q += 2) {
+        chunk(q, W0, W1);
+        chunk(q + 1, W1, W0);
+    }
+    if (q < NQ) chunk(q, W0, W1);
+    // outputs -> LDS (lane chunk of 8*LR words at a 9-granule stride for LR = 4,
+    // conflict-free) -> whole-line 16-B stores of the tile's contiguous output
+    constexpr int GPLo = R * LR / 4;    // output granules per lane
+    constexpr int STR = GPLo + 1;       // padded lane stride (odd)
+    __syncthreads();                    // every wave is done reading the planes
+    uint4 *ob = ug;
+#pragma unroll
+    for (int k = 0; k < GPLo; ++k) {
+        uint32_t w4[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int idx = 4 * k + u, r = idx / LR, o = idx % LR;
+            w4[u] = pack16(limit_t16(yr[o][r], shift), limit_t16(yi[o][r], shift));
+        }
+        ob[t * STR + k] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    }
+    __syncthreads();
+    const long wbase = (long)LR * j0;             // first output word of the tile
+    const long wend = (long)LR * n_total;         // output words of the call
+#pragma unroll
+    for (int i = 0; i < GPLo; ++i) {
+        const int G = i * kUpBlockD + t;          // output granule within the tile
+        const uint4 v = ob[(G / GPLo) * STR + (G % GPLo)];
+        const long w0 = wbase + 4L * G;
+        if (w0 + 4 <= wend) {
+            *(uint4 *)(out + w0) = v;
+        } else {
+            const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+            for (int u = 0; u < 4; ++u)
+                if (w0 + u < wend) out[w0 + u] = vv[u];
+        }
+    }
+}
+
 static int in_bytes(int v) { return v == UV_I16_I32 ? 2 : 4; }
 
 static int up_set(srcdsp_up_state &u, const void *coeffs, int n) {
@@ -223,7 +366,11 @@ static int up_set(srcdsp_up_state &u, const void *coeffs, int n) {
     }
     const int H = n / (int)u.L;
     u.coef_i24 = true;
-    for (int i = 0; i < n; ++i) u.coef_i24 = u.coef_i24 && c[i] < (1 << 23) && c[i] >= -(1 << 23);
+    u.coef_i16 = u.variant == UV_CI16_I32;
+    for (int i = 0; i < n; ++i) {
+        u.coef_i24 = u.coef_i24 && c[i] < (1 << 23) && c[i] >= -(1 << 23);
+        u.coef_i16 = u.coef_i16 && c[i] <= 32767 && c[i] >= -32768;
+    }
     std::vector<int32_t> poly((size_t)n);
     for (unsigned o = 0; o < u.L; ++o)
         for (int i = 0; i < H; ++i) poly[o * H + i] = c[o + i * u.L];
@@ -231,6 +378,19 @@ static int up_set(srcdsp_up_state &u, const void *coeffs, int n) {
     u.d_coef = nullptr;
     SRCDSP_HIP_TRY(hipMalloc(&u.d_coef, 4 * (size_t)n));
     SRCDSP_HIP_TRY(hipMemcpy(u.d_coef, poly.data(), 4 * (size_t)n, hipMemcpyHostToDevice));
+    if (u.d_pair) (void)hipFree(u.d_pair);
+    u.d_pair = nullptr;
+    if (u.coef_i16) {  // tap pairs of each phase: (lo c_o[2p], hi c_o[2p-1]), c_o[-1] = c_o[H] = 0
+        const int Hh = n / (int)u.L, PP = Hh / 2 + 1;
+        std::vector<uint32_t> pr((size_t)u.L * PP);
+        auto tap = [&](unsigned o, int i) {
+            return (i >= 0 && i < Hh) ? (uint32_t)(uint16_t)(int16_t)c[o + (size_t)i * u.L] : 0u;
+        };
+        for (unsigned o = 0; o < u.L; ++o)
+            for (int q = 0; q < PP; ++q) pr[o * PP + q] = tap(o, 2 * q) | (tap(o, 2 * q - 1) << 16);
+        SRCDSP_HIP_TRY(hipMalloc(&u.d_pair, 4 * pr.size()));
+        SRCDSP_HIP_TRY(hipMemcpy(u.d_pair, pr.data(), 4 * pr.size(), hipMemcpyHostToDevice));
+    }
     // buffer.resize(N/L) (:117) keeps the first entries of the ring; a new
     // coefficient set starts from a cleared history here (documented deviation
     // only when H changes and the ring was not reset).
@@ -269,6 +429,25 @@ static int up_launch(srcdsp_up_state &u, const void *d_in, size_t n_in, void *d_
     void *hout0 = u.d_hist[u.cur ^ 1];
     const bool tiled = u.variant != UV_I16_I32 && (u.L == 2 || u.L == 4 || u.L == 8) && u.ntaps <= kUpMaxTaps &&
                        ((uintptr_t)d_in & 15u) == 0 && ((uintptr_t)d_out & 7u) == 0;
+    if (tiled && u.variant == UV_CI16_I32 && u.coef_i16 && (u.L == 2 || u.L == 4) &&
+        ((uintptr_t)d_out & 15u) == 0) {
+        constexpr int TI = kUpRD * kUpBlockD;
+        const int PP = u.H / 2 + 1, HG = (PP + 3) / 4, PGR = TI / 8 + HG;
+        const size_t out_lds = 16 * (size_t)kUpBlockD * (kUpRD * u.L / 4 + 1);  // staged output tile
+        const size_t smem = std::max(4 * 16 * (size_t)PGR, out_lds);
+        const dim3 grid((unsigned)((n_total + TI - 1) / TI));
+        if (u.L == 2)
+            hipLaunchKernelGGL((up_tile_dot2<2>), grid, dim3(kUpBlockD), smem, s, (const uint32_t *)d_in, (long)n_in,
+                               n_total, (const uint32_t *)hin0, (uint32_t *)hout0, u.d_pair, u.H, shift,
+                               (uint32_t *)d_out);
+        else
+            hipLaunchKernelGGL((up_tile_dot2<4>), grid, dim3(kUpBlockD), smem, s, (const uint32_t *)d_in, (long)n_in,
+                               n_total, (const uint32_t *)hin0, (uint32_t *)hout0, u.d_pair, u.H, shift,
+                               (uint32_t *)d_out);
+        SRCDSP_HIP_TRY(hipGetLastError());
+        u.cur ^= 1;
+        return u.order.after(s);
+    }
     if (tiled) {
         constexpr int TI = kUpR * kUpBlock;
         const int NQ = (u.H + 3) / 4;
@@ -355,6 +534,7 @@ SRCDSP_API int srcdsp_up_destroy(srcdsp_up_t h) {
     if (!h) return SRCDSP_OK;
     (void)h->u.order.sync();
     if (h->u.d_coef) (void)hipFree(h->u.d_coef);
+    if (h->u.d_pair) (void)hipFree(h->u.d_pair);
     for (int b = 0; b < 2; ++b)
         if (h->u.d_hist[b]) (void)hipFree(h->u.d_hist[b]);
     h->u.order.destroy();

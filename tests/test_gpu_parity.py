@@ -321,6 +321,26 @@ def test_upsampler_tile_kernel_vs_oracle(S, O, variant, L, H):
         r.reset()
 
 
+@pytest.mark.parametrize("L,H", [(2, 1), (2, 2), (2, 7), (4, 1), (4, 32), (4, 33), (4, 300)])
+def test_upsampler_dot2_kernel_vs_oracle(S, O, L, H):
+    """<ci16,ci16,ci32,int32_t> with int16-range taps (incl. -32768, 32767) runs
+    the v_dot2 interpolator (L = 2, 4); full-scale inputs so the int32
+    accumulators wrap; flush and iterator overloads; uneven chained calls."""
+    rng = np.random.default_rng(100 * L + H)
+    c = rng.integers(-32768, 32768, size=L * H)
+    c[0], c[-1] = -32768, 32767
+    x = O["fma"].gen_ci16(7 * L + H, 0, 0, 40000, -32768, 32767)
+    g = S.FilterUpsamplingFir(c, L, *_UP_TYPES[0])
+    r = O["fma"].up(0, L, c)
+    for it in (False, True):
+        for off, m in _chunks(len(x), [9000, 1, 2049, 4097, 30000]):
+            xs = x[off:off + m]
+            last = off + m >= len(x)
+            assert np.array_equal(g.step(dev(xs), None, last, it).cpu().numpy(), r.step(xs, last, it)), (it, off)
+        g.reset()
+        r.reset()
+
+
 @pytest.mark.parametrize("N,S_", [(1024, 1), (32, 4), (64, 2)])
 def test_correlator_vs_oracle(S, O, N, S_):
     from srcdsp_amd.design import qpsk_pattern
