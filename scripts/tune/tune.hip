@@ -103,14 +103,6 @@ extern "C" int tune_decim(int variant, int grid, const float *d_coef, const void
     hipStream_t s = (hipStream_t)stream;
     auto tiles = [&](int TO) { return (L.n_out + TO - 1) / TO; };
     switch (variant) {
-    case 0: L.ntiles = tiles(256 * 8); return launch(decim_tile_cf32<127, 8, 256, true>, (int)L.ntiles, 256, L, s);
-    case 1: L.ntiles = tiles(256 * 4); return launch(decim_tile_cf32<127, 4, 256, true>, (int)L.ntiles, 256, L, s);
-    case 2: L.ntiles = tiles(128 * 8); return launch(decim_tile_cf32<127, 8, 128, true>, (int)L.ntiles, 128, L, s);
-    case 3: L.ntiles = tiles(256 * 8); return launch(decim_stream_cf32<127, 8, 256, true>, grid, 256, L, s);
-    case 4: L.ntiles = tiles(256 * 4); return launch(decim_stream_cf32<127, 4, 256, true>, grid, 256, L, s);
-    case 5: L.ntiles = tiles(128 * 8); return launch(decim_stream_cf32<127, 8, 128, true>, grid, 128, L, s);
-    case 6: L.ntiles = tiles(64 * 8); return launch(decim_stream_cf32<127, 8, 64, true>, grid, 64, L, s);
-    case 7: L.ntiles = tiles(256 * 6); return launch(decim_stream_cf32<127, 6, 256, true>, grid, 256, L, s);
     // v2: buffer loads + shift-0 quantiser
     case 10: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, false>, grid, 256, L, s);
     case 11: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true>, grid, 256, L, s);

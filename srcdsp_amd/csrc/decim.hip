@@ -7,19 +7,23 @@
 // where x[<0] is the N-1 sample history carried from the previous call.
 //
 // Kernels (decim_kernels.h)
-//  * decim_stream2_cf32<NT,R,BLOCK,FMA,MINW,Q0> -- the headline path:
-//    complex<float>, M = 4, 127/128 taps.  A persistent grid; each workgroup
-//    walks a contiguous run of tiles of BLOCK*R consecutive outputs.  A tile's
-//    input span (4*BLOCK*R samples + the 4*ceil(NT/4) halo) is staged
-//    HBM -> VGPR -> LDS (buffer_load_dwordx4, padded conflict-free layout) and
-//    the NEXT tile's loads are issued before this tile's FMA work.  Each lane
-//    owns R consecutive outputs and walks the taps as 4 polyphase register
-//    windows that slide one sample per 4 taps; taps are wave-uniform SGPR
-//    operands; each output is ONE sequential fma chain in ascending k (FMA) or
-//    separately rounded mul+add (!FMA).
-//  * decim_stream_ci16<NT,R,BLOCK,MIX,MINW> -- complex<int16_t> x int32 taps
-//    (|c| < 2^23: v_mad_i32_i24), same skeleton, optionally with the NCO mixer
-//    of mixers.h fused into the staging pass (config 4).
+//  * decim_stream2_cf32<NT,R,BLOCK,FMA,MINW,Q0,...> -- the headline path:
+//    complex<float>, M = 4, 127/128 taps.  A persistent grid of 512-lane
+//    workgroups taking tiles of BLOCK*R outputs in grid-stride order.  A
+//    tile's input span (4*BLOCK*R samples + the 4*ceil(NT/4) halo) is staged
+//    HBM -> VGPR -> LDS (non-temporal buffer_load_dwordx4, padded
+//    conflict-free layout) and the NEXT tile's loads are issued before this
+//    tile's FMA work.  Each lane owns R consecutive outputs and walks the taps
+//    as 4 polyphase register windows that slide one sample per 4 taps; taps
+//    are wave-uniform SGPR operands; each output is ONE sequential fma chain
+//    in ascending k (FMA) or separately rounded mul+add (!FMA).  Outputs go
+//    back through LDS into whole-line non-temporal stores.
+//  * decim_dot2_ci16<NT,BLOCK,MIX,MINW,TAB2> -- complex<int16_t> x int16-range
+//    taps on v_dot2 tap pairs over planar int16 LDS images, optionally with
+//    the NCO mixer of mixers.h fused into the staging pass (config 4).
+//  * decim_stream_ci16<NT,R,BLOCK,MIX,MINW> -- the same for |c| < 2^23 taps
+//    (v_mad_i32_i24).
+//  * fir_stream_f32 / fir_tile_f32 -- M = 1 (FilterFir) for float input.
 //  * decim_generic<KV,FMA> -- any variant / M / N; one output per thread,
 //    reads through the cache.  Used for shapes without a tile kernel.
 // The new history (last N-1 samples of history ++ input) is written by the

@@ -105,110 +105,6 @@ __global__ void decim_generic(DecimLaunch a, unsigned M) {
     }
 }
 
-// ============================================================ cf32 tiles
-// Tile geometry for complex<float>, M = 4: a granule is 16 B = 2 samples,
-// a 4-sample polyphase group is 2 granules.  LDS granule of tile granule g:
-//   L(g) = g + (g - 2NQ + KPAD*PR) / PR, PR = 2R granules per lane chunk,
-// i.e. one pad granule in front of every lane chunk, so lane t's chunk starts
-// at B_t = 2NQ + KPAD + (2R+1) t and 16 lanes of a ds_read_b128 group hit 16
-// distinct 16-B bank slots.
-template <int NT, int R, int BLOCK, bool FMA>
-__global__ __launch_bounds__(BLOCK) void decim_tile_cf32(DecimLaunch a) {
-    constexpr int NQ = (NT + 3) / 4;
-    constexpr int TO = BLOCK * R;
-    constexpr int TG = 2 * TO + 2 * NQ;
-    constexpr int PR = 2 * R;
-    constexpr int KPAD = ceildiv(2 * NQ, PR);
-    constexpr int LG = TG + (TG + KPAD * PR) / PR + 1;
-    constexpr int PER = ceildiv(TG, BLOCK);
-    __shared__ float4 lds[LG];
-
-    const int ch = blockIdx.y;
-    const float2 *in = (const float2 *)a.in + ch * a.in_stride;
-    const float2 *hist = (const float2 *)a.hist_in[ch];
-    const long n_in = a.n_in;
-    const int H = NT - 1;
-    const long tile = xcd_tile(blockIdx.x, gridDim.x);
-    const long o0 = tile * TO;
-    const long b0 = 4 * o0 - 4 * NQ;
-    const int t = threadIdx.x;
-
-    if (tile == 0) write_history(in, n_in, hist, (float2 *)a.hist_out[ch], H);
-
-    // ---- stage the tile: HBM -> VGPR -> LDS (all loads issued before any write)
-    float4 v[PER];
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int g = t + i * BLOCK;
-        const long s = b0 + 2 * (long)g;
-        if (g < TG) {
-            if (s >= 0 && s + 1 < n_in) {
-                v[i] = *(const float4 *)(in + s);
-            } else {
-                float2 lo = fetch(in, hist, s, n_in, H), hi = fetch(in, hist, s + 1, n_in, H);
-                v[i] = make_float4(lo.x, lo.y, hi.x, hi.y);
-            }
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int g = t + i * BLOCK;
-        if (g < TG) lds[g + (g - 2 * NQ + KPAD * PR) / PR] = v[i];
-    }
-    __syncthreads();
-
-    // ---- compute: lane t owns outputs n0 .. n0+R-1
-    const int Bt = 2 * NQ + KPAD + (PR + 1) * t;
-    ConstPtr<float> tp = const_view<float>(a.coef);
-    float2 X[4 * (NQ + R)];  // X[s + 4NQ] = x[4 n0 + s]
-    float yr[R], yi[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) yr[r] = yi[r] = 0.f;
-
-    auto load_group = [&](int e) {  // samples 4e .. 4e+3 relative to 4 n0
-        const float4 g0 = lds[Bt + 2 * e + floordiv(2 * e, PR)];
-        const float4 g1 = lds[Bt + 2 * e + 1 + floordiv(2 * e + 1, PR)];
-        X[4 * e + 4 * NQ + 0] = make_float2(g0.x, g0.y);
-        X[4 * e + 4 * NQ + 1] = make_float2(g0.z, g0.w);
-        X[4 * e + 4 * NQ + 2] = make_float2(g1.x, g1.y);
-        X[4 * e + 4 * NQ + 3] = make_float2(g1.z, g1.w);
-    };
-#pragma unroll
-    for (int e = -1; e < R; ++e) load_group(e);
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        if (q + 1 < NQ) load_group(-q - 2);
-        if ((q & 3) == 0) asm volatile("" : "+s"(tp));
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            const int k = 4 * q + p;
-            if (k < NT) {
-                const float c = tp[k];
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const float2 x = X[4 * (r - q) - p + 4 * NQ];
-                    yr[r] = mac<FMA>(c, x.x, yr[r]);
-                    yi[r] = mac<FMA>(c, x.y, yi[r]);
-                }
-            }
-        }
-    }
-
-    // ---- quantise (limitScale16) and store
-    float2 *out = (float2 *)a.out + ch * a.out_stride;
-    const long n0 = o0 + (long)t * R;
-    const unsigned sh = a.shift;
-    if (n0 + R <= a.n_out && (R % 2) == 0) {
-#pragma unroll
-        for (int r = 0; r < R; r += 2)
-            *(float4 *)(out + n0 + r) = make_float4(q16f(yr[r], sh), q16f(yi[r], sh), q16f(yr[r + 1], sh),
-                                                    q16f(yi[r + 1], sh));
-    } else {
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-            if (n0 + r < a.n_out) out[n0 + r] = make_float2(q16f(yr[r], sh), q16f(yi[r], sh));
-    }
-}
 
 // ============================================================ ci16 tiles
 // complex<int16_t> samples are 4 B, so a 4-sample polyphase group is one
@@ -239,115 +135,6 @@ namespace srcdsp {
 // next tile's prefetch) and output stores stay in flight across the barrier.
 #define SRCDSP_LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 
-// Persistent variant of decim_tile_cf32: gridDim.x workgroups each own a
-// contiguous run of tiles (XCD-aware order of the runs) and software-pipeline
-// them -- the HBM loads of tile k+1 are issued into VGPRs right after tile k
-// is written to LDS, so their latency hides under tile k's FMA work.
-template <int NT, int R, int BLOCK, bool FMA, int MINW = 1>
-__global__ __launch_bounds__(BLOCK, MINW) void decim_stream_cf32(DecimLaunch a) {
-    constexpr int NQ = (NT + 3) / 4;
-    constexpr int TO = BLOCK * R;
-    constexpr int TG = 2 * TO + 2 * NQ;
-    constexpr int PR = 2 * R;
-    constexpr int KPAD = ceildiv(2 * NQ, PR);
-    constexpr int LG = TG + (TG + KPAD * PR) / PR + 1;
-    constexpr int PER = ceildiv(TG, BLOCK);
-    __shared__ float4 lds[LG];
-
-    const int ch = blockIdx.y;
-    const float2 *in = (const float2 *)a.in + ch * a.in_stride;
-    const float2 *hist = (const float2 *)a.hist_in[ch];
-    float2 *out = (float2 *)a.out + ch * a.out_stride;
-    const long n_in = a.n_in;
-    const int H = NT - 1;
-    const int t = threadIdx.x;
-    const long nb = gridDim.x;
-    const long b = xcd_tile(blockIdx.x, nb);
-    const long per = a.ntiles / nb, rem = a.ntiles % nb;
-    const long t_begin = b * per + (b < rem ? b : rem);
-    const long t_end = t_begin + per + (b < rem ? 1 : 0);
-    if (t_begin == 0 && t_end > 0) write_history(in, n_in, hist, (float2 *)a.hist_out[ch], H);
-
-    float4 v[PER];
-    auto stage_load = [&](long tile) {
-        const long b0 = 4 * tile * TO - 4 * NQ;
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int g = t + i * BLOCK;
-            const long s = b0 + 2 * (long)g;
-            if (g < TG) {
-                if (s >= 0 && s + 1 < n_in) {
-                    v[i] = *(const float4 *)(in + s);
-                } else {
-                    float2 lo = fetch(in, hist, s, n_in, H), hi = fetch(in, hist, s + 1, n_in, H);
-                    v[i] = make_float4(lo.x, lo.y, hi.x, hi.y);
-                }
-            }
-        }
-    };
-    if (t_begin < t_end) stage_load(t_begin);
-    const int Bt = 2 * NQ + KPAD + (PR + 1) * t;
-    for (long tile = t_begin; tile < t_end; ++tile) {
-        SRCDSP_LDS_BARRIER();  // every wave is done reading the previous tile
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int g = t + i * BLOCK;
-            if (g < TG) lds[g + (g - 2 * NQ + KPAD * PR) / PR] = v[i];
-        }
-        SRCDSP_LDS_BARRIER();
-        if (tile + 1 < t_end) stage_load(tile + 1);
-
-        // re-read the taps from the constant kernarg segment every tile: an
-        // opaque per-iteration pointer stops the compiler from hoisting all
-        // NT scalar loads out of the loop (that would spill SGPRs to VGPRs)
-        ConstPtr<float> tp = const_view<float>(a.coef);
-        asm volatile("" : "+s"(tp));
-        float2 X[4 * (NQ + R)];
-        float yr[R], yi[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) yr[r] = yi[r] = 0.f;
-        auto load_group = [&](int e) {
-            const float4 g0 = lds[Bt + 2 * e + floordiv(2 * e, PR)];
-            const float4 g1 = lds[Bt + 2 * e + 1 + floordiv(2 * e + 1, PR)];
-            X[4 * e + 4 * NQ + 0] = make_float2(g0.x, g0.y);
-            X[4 * e + 4 * NQ + 1] = make_float2(g0.z, g0.w);
-            X[4 * e + 4 * NQ + 2] = make_float2(g1.x, g1.y);
-            X[4 * e + 4 * NQ + 3] = make_float2(g1.z, g1.w);
-        };
-#pragma unroll
-        for (int e = -1; e < R; ++e) load_group(e);
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            if (q + 1 < NQ) load_group(-q - 2);
-            if ((q & 3) == 0) asm volatile("" : "+s"(tp));  // taps fetched 16 at a time
-#pragma unroll
-            for (int p = 0; p < 4; ++p) {
-                const int k = 4 * q + p;
-                if (k < NT) {
-                    const float c = tp[k];
-#pragma unroll
-                    for (int r = 0; r < R; ++r) {
-                        const float2 x = X[4 * (r - q) - p + 4 * NQ];
-                        yr[r] = mac<FMA>(c, x.x, yr[r]);
-                        yi[r] = mac<FMA>(c, x.y, yi[r]);
-                    }
-                }
-            }
-        }
-        const long n0 = tile * TO + (long)t * R;
-        const unsigned sh = a.shift;
-        if (n0 + R <= a.n_out && (R % 2) == 0) {
-#pragma unroll
-            for (int r = 0; r < R; r += 2)
-                *(float4 *)(out + n0 + r) = make_float4(q16f(yr[r], sh), q16f(yi[r], sh), q16f(yr[r + 1], sh),
-                                                        q16f(yi[r + 1], sh));
-        } else {
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-                if (n0 + r < a.n_out) out[n0 + r] = make_float2(q16f(yr[r], sh), q16f(yi[r], sh));
-        }
-    }
-}
 
 }  // namespace srcdsp
 namespace srcdsp {
@@ -363,7 +150,18 @@ __device__ __forceinline__ float q16f_shift0(float y) {
     return __builtin_fabsf(y) < 2147483648.0f ? t : 0.0f;
 }
 
-// Persistent cf32 decimator, v2: as decim_stream_cf32, plus
+// Persistent complex<float> decimator, M = 4 (the headline, a1).
+// A tile is BLOCK*R outputs; its input span (4*BLOCK*R samples + a 4*NQ
+// sample halo, NQ = ceil(NT/4)) is staged HBM -> VGPR -> LDS as 16-B granules
+// (2 samples).  LDS granule of tile granule g:
+//   L(g) = g + (g - 2NQ + KPAD*PR) / PR,  PR = 2R granules per lane chunk,
+// i.e. one pad granule in front of every lane chunk, so lane t's chunk starts
+// at B_t = 2NQ + KPAD + (2R+1) t and the 16 lanes of a ds_read_b128 group hit
+// 16 distinct 16-B bank slots.  Each lane owns R consecutive outputs and walks
+// the taps as 4 polyphase register windows sliding one sample per 4 taps;
+// taps are wave-uniform SGPR operands through a constant view.  Persistent:
+// the next tile's loads are issued into VGPRs right after the current tile
+// lands in LDS.  Plus:
 //  * buffer_load_dwordx4 staging through a per-tile buffer descriptor
 //    (32-bit lane offsets, hardware range check returns 0 past the input end,
 //    so the tail needs no per-lane compare) -- fewer VALU ops per load;
@@ -372,7 +170,8 @@ __device__ __forceinline__ float q16f_shift0(float y) {
 // 2 = compute path only (every tile reads the same L2-resident input span)
 // NTL: non-temporal (streaming) input loads; OST: outputs staged through LDS
 // so each store instruction writes whole contiguous lines; NTS: non-temporal
-// output stores.
+// output stores; GS: grid-stride tile order (else a contiguous run of tiles
+// per workgroup); PF2: two tiles in flight (two register sets).
 template <bool NTS>
 __device__ __forceinline__ void store16(float4 *p, float4 v) {
     if constexpr (NTS) {
