@@ -137,6 +137,13 @@ extern "C" int tune_decim(int variant, int grid, const float *d_coef, const void
     case 50: L.ntiles = tiles(1024 * 4); return launch(decim_stream2_cf32<127, 4, 1024, true, 4, true, 0, true, true, true, true>, grid, 1024, L, s);
     case 51: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, false>, grid, 512, L, s);
     case 52: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, false, true, true, true>, grid, 512, L, s);
+    case 60: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, false, 2, 2>, grid, 512, L, s);
+    case 61: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, false, 2, 3>, grid, 512, L, s);
+    case 62: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, false, 3, 2>, grid, 512, L, s);
+    case 63: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, false, 3, 3>, grid, 512, L, s);
+    case 64: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, false, 18, 18>, grid, 512, L, s);
+    case 65: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, false, 2, 19>, grid, 512, L, s);
+    case 66: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, false, 19, 2>, grid, 512, L, s);
     case 24: L.ntiles = tiles(128 * 8); return launch(decim_stream2_cf32<127, 8, 128, true, 2, true>, grid, 128, L, s);
     default: return -1;
     }

@@ -74,7 +74,9 @@ def main():
             fn()
             med, mn = timeit(fn, 10)
             print(f"  {label}, {blocks} blocks: {mn:.4f} ms -> {bps * L / (mn * 1e-3) / 1e9:.1f} GB/s")
-    variants = [(48, 1024, "B512 g1024 (product)"), (42, 2048, "B256 g2048 (previous)")]
+    variants = [(48, 1024, "product (nt/nt builtin)"), (60, 1024, "ld 2 st 2 (buffer)"), (61, 1024, "ld 2 st 3"),
+                (62, 1024, "ld 3 st 2"), (63, 1024, "ld 3 st 3"), (64, 1024, "ld 18 st 18"), (65, 1024, "ld 2 st 19"),
+                (66, 1024, "ld 19 st 2")]
     if os.environ.get("TUNE_SUSTAINED_ONLY"):
         sustained_rounds(variants, x, y, cdev, h0, h1, stream, L, ref)
         return

@@ -183,7 +183,7 @@ __device__ __forceinline__ void store16(float4 *p, float4 v) {
     }
 }
 template <int NT, int R, int BLOCK, bool FMA, int MINW, bool Q0, int PROBE = 0, bool NTL = false, bool OST = false,
-          bool NTS = false, bool GS = false, bool PF2 = false>
+          bool NTS = false, bool GS = false, bool PF2 = false, int LAUX = -1, int SAUX = -1>
 __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a) {
     constexpr int NQ = (NT + 3) / 4;
     constexpr int TO = BLOCK * R;
@@ -224,7 +224,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
         for (int i = 0; i < PER; ++i) {
             const int g = t + i * BLOCK;
             if (g < TG) {
-                auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * g, 0, NTL ? 2 : 0);  // aux 2 = nt
+                // aux: bit0 sc0, bit1 nt, bit4 sc1 (LAUX >= 0: tuning override)
+                auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * g, 0, LAUX >= 0 ? LAUX : (NTL ? 2 : 0));
                 v[i] = make_float4(__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]),
                                    __uint_as_float(w[3]));
             }
@@ -319,7 +320,17 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
 #pragma unroll
                 for (int i = 0; i < TO / 2 / BLOCK; ++i) {
                     const int k = t + i * BLOCK;
-                    store16<NTS>((float4 *)(out + o0 + 2 * k), ob4[k]);
+                    if constexpr (SAUX >= 0) {  // tuning override of the store policy
+                        __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+                            (void *)(out + o0), 0, 0x7ffffff0, 0x00020000);
+                        const float4 v4 = ob4[k];
+                        typedef unsigned u4_t __attribute__((ext_vector_type(4)));
+                        const u4_t u = {__float_as_uint(v4.x), __float_as_uint(v4.y), __float_as_uint(v4.z),
+                                        __float_as_uint(v4.w)};
+                        __builtin_amdgcn_raw_buffer_store_b128(u, ro, 16 * k, 0, SAUX);
+                    } else {
+                        store16<NTS>((float4 *)(out + o0 + 2 * k), ob4[k]);
+                    }
                 }
             } else {
                 for (int k = t; k < TO; k += BLOCK)
