@@ -53,6 +53,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=1 << 27, help="samples timed on the reference CPU path")
     p.add_argument("--no-gather", action="store_true")
+    p.add_argument("--no-pcie", action="store_true", help="skip the host-vector (PCIe-inclusive) side measurement")
     p.add_argument("--dump-steps", action="store_true", help="print every timed step's kernel ms to stderr")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return p.parse_args()
@@ -331,6 +332,26 @@ def cpu_baseline_other(args, pyoracle):
                       f"host CPU: {_cpu_model()}"}
 
 
+def pcie_inclusive(S):
+    """The reference-style host std::vector step() (srcdsp_decim_step_host):
+    host input staged through pinned memory, H2D, the same kernel, D2H.  A side
+    figure, never `value`."""
+    from srcdsp_amd.design import hamming_sinc
+    n = 1 << 26
+    x = np.random.default_rng(0).integers(-2048, 2048, size=(n, 2)).astype(np.float32).view(np.complex64).reshape(n)
+    y = np.empty(n // 4, np.complex64)
+    f = S.FilterDnsamplingFir(hamming_sinc(127), 4)
+    f.step(x, y)  # warm (pinned staging allocation)
+    t0 = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        f.step(x, y)
+    secs = (time.perf_counter() - t0) / reps
+    return {"value": round(n / secs / 1e6, 1), "unit": "Msamples/s",
+            "sample": f"{n} samples per host-vector step(), mean of {reps}: memcpy to pinned, H2D, kernel, "
+                      "D2H, memcpy out (10 B/sample over PCIe)"}
+
+
 def pmc_traffic(args, work_name, per_launch_samples):
     """Per-launch HBM bytes from the committed rocprofv3 PMC summary (see
     profiles/README.md for how it is collected and corrected), if it matches."""
@@ -436,6 +457,8 @@ def main():
             line["detection"] = list(work.last)
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(args)
+        if args.workload == "decim" and world == 1 and not args.no_pcie:
+            line["pcie_inclusive"] = pcie_inclusive(S)
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist
