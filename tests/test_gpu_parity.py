@@ -434,3 +434,39 @@ def test_time_split_segments_equal_single_call(S, O):
         if found:
             assert np.array_equal(owner.getRefBitSamples(), bits)
     del torch
+
+
+def test_mixer_decimator_correlator_pipeline_device_resident(S, O):
+    """the chained mixer -> decimator -> correlator pipeline with
+    device-resident intermediates (the decimated stream never leaves HBM):
+    same detection, index and bitSamples as the three oracle calls."""
+    from srcdsp_amd.design import hamming_sinc, q14, qpsk_pattern
+    rng = np.random.default_rng(8)
+    p = qpsk_pattern(64, 300, seed=4)
+    # a baseband stream whose decimated output carries the pattern
+    n = 1 << 18
+    x = rng.integers(-500, 500, size=(n, 2))
+    at = 150000
+    x[at:at + 4 * 64] += 40 * np.repeat(p, 4, axis=0)  # each symbol held for M = 4 inputs
+    x = np.clip(x, -32768, 32767).astype(np.int16)
+    cq = q14(hamming_sinc(127, 0.12))
+    m = S.Mixer(4096)
+    m.reset(0.0)
+    chain = S.MixerDecimatorChain(m, S.FilterDnsamplingFir(cq, 4, "complex<int16_t>", "complex<int16_t>",
+                                                           "complex<int32_t>", "int32_t"))
+    g = S.FixedPatternCorrelator(64, 1)
+    g.setPattern(p)
+    om, od, oc = O["fma"].mixer(4096), O["fma"].decim(1, 4, cq), O["fma"].corr(64, 1)
+    om.reset(0.0)
+    oc.set_pattern(p)
+    xd = dev(x)
+    hits = []
+    for off in range(0, n, 1 << 16):  # four blocks, state carried on the device
+        y = chain.step(xd[off:off + (1 << 16)])
+        assert y.is_cuda
+        hits.append(g.step(y))
+        exp = oc.step(od.step(om.step(x[off:off + (1 << 16)])))
+        assert hits[-1][0] == exp[0] and (not exp[0] or hits[-1][1] == exp[1]), (off, hits[-1], exp)
+        if exp[0]:
+            assert np.array_equal(g.getRefBitSamples(), oc.bit_samples())
+    assert sum(h[0] for h in hits) == 1  # the pattern is found once, in the third block
