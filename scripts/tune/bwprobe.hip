@@ -95,6 +95,34 @@ __global__ __launch_bounds__(256) void aux_probe(const float4_t *in, float4_t *o
     }
 }
 
+// Output bursts: each block reduces K chunks (64 KiB in -> 16 KiB out each)
+// into LDS, then writes the K*16 KiB as one contiguous burst.  Chunks are
+// taken in grid-stride order of K-chunk super tiles.  Tests whether fewer,
+// larger write bursts ease the HBM read/write turnaround of the 4:1 mix.
+template <int K, bool NTL, bool NTS>
+__global__ __launch_bounds__(256) void burst_probe(const float4_t *in, float4_t *out, long n_out) {
+    __shared__ float4_t ob[K * 1024];
+    const int t = threadIdx.x;
+    const long nsuper = n_out / (K * 1024);
+    for (long s = blockIdx.x; s < nsuper; s += gridDim.x) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const long o0 = (s * K + k) * 1024;  // first output granule of the chunk
+            float4_t v[16];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[4 * u + r] = ld<NTL>(in + 4 * o0 + u * 1024 + r * 256 + t);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) ob[k * 1024 + u * 256 + t] = v[4 * u] + v[4 * u + 1] + v[4 * u + 2] + v[4 * u + 3];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 4 * K; ++i) st<NTS>(out + s * K * 1024 + i * 256 + t, ob[i * 256 + t]);
+        __syncthreads();
+    }
+}
+
 __global__ __launch_bounds__(256) void fill_probe(float4_t *out, long n) {
     const long nth = (long)gridDim.x * 256;
     const float4_t z = {1, 2, 3, 4};
@@ -137,6 +165,13 @@ extern "C" int bw_probe(int id, int blocks, const void *in_, void *out_, long n_
     case 20:
         hipLaunchKernelGGL(fill_probe, dim3(blocks), dim3(256), 0, s, out, n_in16 / 4);
         break;
+        CASE(13, 4, 2, true, true, true)    // 4:1 contiguous, nt both
+#define BCASE(id, K, NL, NS)                                                                          \
+    case id:                                                                                         \
+        hipLaunchKernelGGL((burst_probe<K, NL, NS>), dim3(blocks), dim3(256), 0, s, in, out, n_in16 / 4); \
+        break;
+        BCASE(40, 1, true, true) BCASE(41, 2, true, true) BCASE(42, 4, true, true) BCASE(43, 8, true, true)
+        BCASE(44, 4, true, false)
     default:
         return -1;
     }

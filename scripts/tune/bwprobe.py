@@ -35,6 +35,17 @@ def main():
         for k, la in enumerate((1, 3, 16, 17, 18, 19)):
             CASES[120 + k] = (f"4:1 contig ld aux {la} st aux 2", 4)
         grids = (1024, 2048)
+    if os.environ.get("BW_BURST"):
+        CASES.clear()
+        CASES.update({13: ("4:1 contig U2 nt-both", 4), 5: ("4:1 gs U2 nt-both", 4),
+                      40: ("4:1 burst K1 nt-both", 4), 41: ("4:1 burst K2 nt-both", 4),
+                      42: ("4:1 burst K4 nt-both", 4), 43: ("4:1 burst K8 nt-both", 4),
+                      44: ("4:1 burst K4 nt-load", 4), 10: ("read-only U2 nt", 0), 20: ("write-only fill", -1)})
+        grids = (512, 1024, 2048, 4096)
+    off_g = int(os.environ.get("BW_OUT_OFFSET", "0"))  # output base offset in 16-B granules
+    if off_g:
+        y = torch.empty(n16 * 4 + off_g * 4, dtype=torch.float32, device="cuda")[off_g * 4:]
+        print(f"output base offset: {off_g * 16} B (address {y.data_ptr():#x}, input {x.data_ptr():#x})")
     for rnd in range(4):
         for cid in CASES:
             for g in grids:

@@ -129,21 +129,22 @@ extern "C" int tune_decim(int variant, int grid, const float *d_coef, const void
     case 42: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 0, true, true, true, true>, grid, 256, L, s);
     case 43: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 1, false, false, false, true>, grid, 256, L, s);
     case 44: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 0, false, true, true, true>, grid, 256, L, s);
-    case 45: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 3, true, 0, true, true, true, true, true>, grid, 256, L, s);
-    case 46: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 0, true, true, true, true, true>, grid, 256, L, s);
-    case 47: L.ntiles = tiles(128 * 4); return launch(decim_stream2_cf32<127, 4, 128, true, 6, true, 0, true, true, true, true, true>, grid, 128, L, s);
     case 48: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true>, grid, 512, L, s);
     case 49: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 3, true, 0, true, true, true, true>, grid, 512, L, s);
     case 50: L.ntiles = tiles(1024 * 4); return launch(decim_stream2_cf32<127, 4, 1024, true, 4, true, 0, true, true, true, true>, grid, 1024, L, s);
     case 51: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, false>, grid, 512, L, s);
     case 52: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, false, true, true, true>, grid, 512, L, s);
-    case 60: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, false, 2, 2>, grid, 512, L, s);
-    case 61: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, false, 2, 3>, grid, 512, L, s);
-    case 62: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, false, 3, 2>, grid, 512, L, s);
-    case 63: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, false, 3, 3>, grid, 512, L, s);
-    case 64: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, false, 18, 18>, grid, 512, L, s);
-    case 65: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, false, 2, 19>, grid, 512, L, s);
-    case 66: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, false, 19, 2>, grid, 512, L, s);
+    case 60: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, 2, 2>, grid, 512, L, s);
+    case 61: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, 2, 3>, grid, 512, L, s);
+    case 62: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, 3, 2>, grid, 512, L, s);
+    case 63: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, 3, 3>, grid, 512, L, s);
+    case 64: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, 18, 18>, grid, 512, L, s);
+    case 65: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, 2, 19>, grid, 512, L, s);
+    case 66: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, 19, 2>, grid, 512, L, s);
+    case 80: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 1, true, true, true, true>, grid, 512, L, s);
+    case 84: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 1, true, true, true, true>, grid, 256, L, s);
+    case 88: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 0, true, true, true, true>, grid, 256, L, s);
+    case 90: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 2, true, 1, true, true, true, true>, grid, 512, L, s);
     case 24: L.ntiles = tiles(128 * 8); return launch(decim_stream2_cf32<127, 8, 128, true, 2, true>, grid, 128, L, s);
     default: return -1;
     }

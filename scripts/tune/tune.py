@@ -15,7 +15,19 @@ from srcdsp_amd.design import hamming_sinc  # noqa: E402
 import srcdsp_amd as S  # noqa: E402
 
 lib = C.CDLL(os.path.join(HERE, "libtune.so"))
+_old = os.path.join(HERE, "libtune_old.so")  # optional A/B baseline: the previous headline kernel
+lib_old = C.CDLL(_old) if os.path.exists(_old) else None
+
+
+def tune_decim(variant, grid, *args):
+    """variant < 0: the previous headline kernel from libtune_old.so"""
+    if variant < 0:
+        return lib_old.tune_decim_old(grid, *args)
+    return lib.tune_decim(variant, grid, *args)
 lib.tune_fma_rate.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+if lib_old is not None:
+    lib_old.tune_decim_old.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_long, C.c_void_p,
+                                       C.c_void_p, C.c_void_p]
 lib.tune_decim.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_long, C.c_void_p,
                            C.c_void_p, C.c_void_p]
 
@@ -77,13 +89,17 @@ def main():
     variants = [(48, 1024, "product (nt/nt builtin)"), (60, 1024, "ld 2 st 2 (buffer)"), (61, 1024, "ld 2 st 3"),
                 (62, 1024, "ld 3 st 2"), (63, 1024, "ld 3 st 3"), (64, 1024, "ld 18 st 18"), (65, 1024, "ld 2 st 19"),
                 (66, 1024, "ld 19 st 2")]
+    if os.environ.get("TUNE_OCC"):  # workgroups per CU; PROBE1 = memory path only (no correctness check)
+        variants = [(-1, 1024, "previous head g1024"), (48, 1024, "head g1024"), (48, 512, "head g512"),
+                    (80, 1024, "PROBE1 512 g1024"), (80, 512, "PROBE1 512 g512"), (90, 256, "PROBE1 512 mw2 g256"),
+                    (84, 1024, "PROBE1 256 g1024"), (88, 1024, "256 lanes g1024")]
     if os.environ.get("TUNE_SUSTAINED_ONLY"):
         sustained_rounds(variants, x, y, cdev, h0, h1, stream, L, ref)
         return
     res = {v: [] for v in variants}
     for rnd in range(int(os.environ.get('TUNE_ROUNDS', '6'))):
         for v in variants:
-            fn = lambda: lib.tune_decim(v[0], v[1], C.c_void_p(cdev.data_ptr()), C.c_void_p(x.data_ptr()),
+            fn = lambda: tune_decim(v[0], v[1], C.c_void_p(cdev.data_ptr()), C.c_void_p(x.data_ptr()),
                                         C.c_void_p(y.data_ptr()), L, C.c_void_p(h0.data_ptr()),
                                         C.c_void_p(h1.data_ptr()), stream)
             if rnd == 0:
@@ -109,8 +125,10 @@ def sustained_rounds(variants, x, y, cdev, h0, h1, stream, L, ref, rounds=4, rep
     round and variant the median of the last 20 launches; min/median over rounds."""
     res = {v: [] for v in variants}
     for v in variants:  # correctness first
+        if "PROBE" in v[2]:
+            continue
         y.zero_()
-        lib.tune_decim(v[0], v[1], C.c_void_p(cdev.data_ptr()), C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()),
+        tune_decim(v[0], v[1], C.c_void_p(cdev.data_ptr()), C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()),
                        L, C.c_void_p(h0.data_ptr()), C.c_void_p(h1.data_ptr()), stream)
         torch.cuda.synchronize()
         assert torch.equal(y.view(torch.int32), ref.view(torch.int32)), v
@@ -120,7 +138,7 @@ def sustained_rounds(variants, x, y, cdev, h0, h1, stream, L, ref, rounds=4, rep
             ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
             for i in range(reps):
                 ev[i][0].record(st)
-                lib.tune_decim(v[0], v[1], C.c_void_p(cdev.data_ptr()), C.c_void_p(x.data_ptr()),
+                tune_decim(v[0], v[1], C.c_void_p(cdev.data_ptr()), C.c_void_p(x.data_ptr()),
                                C.c_void_p(y.data_ptr()), L, C.c_void_p(h0.data_ptr()), C.c_void_p(h1.data_ptr()),
                                stream)
                 ev[i][1].record(st)
@@ -140,7 +158,7 @@ def sustained(variants, x, y, cdev, h0, h1, stream, L, reps=60):
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
         for i in range(reps):
             ev[i][0].record(st)
-            lib.tune_decim(v[0], v[1], C.c_void_p(cdev.data_ptr()), C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()),
+            tune_decim(v[0], v[1], C.c_void_p(cdev.data_ptr()), C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()),
                            L, C.c_void_p(h0.data_ptr()), C.c_void_p(h1.data_ptr()), stream)
             ev[i][1].record(st)
         torch.cuda.synchronize()

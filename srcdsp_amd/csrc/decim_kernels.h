@@ -171,7 +171,7 @@ __device__ __forceinline__ float q16f_shift0(float y) {
 // NTL: non-temporal (streaming) input loads; OST: outputs staged through LDS
 // so each store instruction writes whole contiguous lines; NTS: non-temporal
 // output stores; GS: grid-stride tile order (else a contiguous run of tiles
-// per workgroup); PF2: two tiles in flight (two register sets).
+// per workgroup).
 template <bool NTS>
 __device__ __forceinline__ void store16(float4 *p, float4 v) {
     if constexpr (NTS) {
@@ -183,7 +183,7 @@ __device__ __forceinline__ void store16(float4 *p, float4 v) {
     }
 }
 template <int NT, int R, int BLOCK, bool FMA, int MINW, bool Q0, int PROBE = 0, bool NTL = false, bool OST = false,
-          bool NTS = false, bool GS = false, bool PF2 = false, int LAUX = -1, int SAUX = -1>
+          bool NTS = false, bool GS = false, int LAUX = -1, int SAUX = -1>
 __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a) {
     constexpr int NQ = (NT + 3) / 4;
     constexpr int TO = BLOCK * R;
@@ -212,7 +212,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
     const long t_step = GS ? nb : kStep1;
     if (t_begin == 0 && t_end > 0) write_history(in, n_in, hist, (float2 *)a.hist_out[ch], H);
 
-    float4 v[PER], v2[PER];
+    float4 v[PER];
     // tiles >= 1: one descriptor per tile, 32-bit lane offsets, range-checked
     auto stage_load = [&](float4 (&v)[PER], long tile) {
         if constexpr (PROBE == 2) tile = 1 + (tile & 15);
@@ -225,7 +225,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
             const int g = t + i * BLOCK;
             if (g < TG) {
                 // aux: bit0 sc0, bit1 nt, bit4 sc1 (LAUX >= 0: tuning override)
-                auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * g, 0, LAUX >= 0 ? LAUX : (NTL ? 2 : 0));
+                // lane offset in the VGPR, the per-load step in soffset (an
+                // SGPR constant): one offset VGPR for all PER loads
+                auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * t, 16 * i * BLOCK,
+                                                              LAUX >= 0 ? LAUX : (NTL ? 2 : 0));
                 v[i] = make_float4(__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]),
                                    __uint_as_float(w[3]));
             }
@@ -246,12 +249,11 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
         } else {
             stage_load(v, t_begin);
         }
-        if (PF2 && t_begin + t_step < t_end) stage_load(v2, t_begin + t_step);
     }
     const int Bt = 2 * NQ + KPAD + (PR + 1) * t;
-    // PF2: two register sets alternate (tiles k and k+1 in flight while k is
-    // computed); otherwise one set, refilled right after it lands in LDS
-    auto do_tile = [&](long tile, float4 (&v)[PER]) {
+    // the staged tile lands in LDS once every wave is done with the previous
+    // tile's image (and its output staging, which reuses it)
+    auto stage_to_lds = [&]() {
         SRCDSP_LDS_BARRIER();
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
@@ -259,11 +261,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
             if (g < TG) lds[g + (g - 2 * NQ + KPAD * PR) / PR] = v[i];
         }
         SRCDSP_LDS_BARRIER();
-        if (PF2) {
-            if (tile + 2 * t_step < t_end) stage_load(v, tile + 2 * t_step);
-        } else if (tile + t_step < t_end) {
-            stage_load(v, tile + t_step);
-        }
+    };
+    // one tile: taps over the LDS image, outputs stored.  The loop below
+    // issues the next tile's loads before this and lands them in LDS after
+    // it, all in one iteration: the compiler then waits for the loads with
+    // vmcnt(this tile's stores) and the stores stay in flight.
+    auto do_tile = [&](long tile) {
 
         ConstPtr<float> tp = const_view<float>(a.coef);
         asm volatile("" : "+s"(tp));
@@ -346,13 +349,13 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
                 if (n0 + r < a.n_out) out[n0 + r] = make_float2(q(yr[r]), q(yi[r]));
         }
         };
-    if constexpr (PF2) {
-        for (long tile = t_begin; tile < t_end; tile += 2 * t_step) {
-            do_tile(tile, v);
-            if (tile + t_step < t_end) do_tile(tile + t_step, v2);
-        }
-    } else {
-        for (long tile = t_begin; tile < t_end; tile += t_step) do_tile(tile, v);
+    if (t_begin < t_end) stage_to_lds();
+    for (long tile = t_begin; tile < t_end;) {
+        const long nxt = tile + t_step;
+        if (nxt < t_end) stage_load(v, nxt);
+        do_tile(tile);
+        if (nxt < t_end) stage_to_lds();
+        tile = nxt;
     }
 
 }
