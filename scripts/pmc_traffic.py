@@ -61,7 +61,7 @@ def main():
     ap.add_argument("--samples", type=int, default=1 << 28)
     a = ap.parse_args()
     key = KERNEL_KEYS[a.workload]
-    bench_args = ["--workload", a.workload, "--steps", "5", "--warmup", "1", "--no-cpu-baseline",
+    bench_args = ["--workload", a.workload, "--steps", "5", "--warmup", "1", "--no-cpu-baseline", "--no-pcie",
                   "--samples", str(a.samples)]
     res = {}
     for i, counters in enumerate(PASSES):

@@ -92,7 +92,8 @@ def main():
     if os.environ.get("TUNE_OCC"):  # workgroups per CU; PROBE1 = memory path only (no correctness check)
         variants = [(-1, 1024, "previous head g1024"), (48, 1024, "head g1024"), (48, 512, "head g512"),
                     (80, 1024, "PROBE1 512 g1024"), (80, 512, "PROBE1 512 g512"), (90, 256, "PROBE1 512 mw2 g256"),
-                    (84, 1024, "PROBE1 256 g1024"), (88, 1024, "256 lanes g1024")]
+                    (84, 1024, "PROBE1 256 g1024"), (88, 1024, "256 lanes g1024"), (48, 1024, "head g1024 (again)"),
+                    (-1, 1024, "previous head g1024 (again)")]
     if os.environ.get("TUNE_SUSTAINED_ONLY"):
         sustained_rounds(variants, x, y, cdev, h0, h1, stream, L, ref)
         return
