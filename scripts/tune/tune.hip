@@ -145,6 +145,16 @@ extern "C" int tune_decim(int variant, int grid, const float *d_coef, const void
     case 84: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 1, true, true, true, true>, grid, 256, L, s);
     case 88: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 0, true, true, true, true>, grid, 256, L, s);
     case 90: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 2, true, 1, true, true, true, true>, grid, 512, L, s);
+    // compute path only (PROBE=2: every tile re-reads one of 16 L2-resident spans)
+    case 110: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 2, true, true, true, true>, grid, 512, L, s);
+    case 111: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 2, true, 2, true, true, true, true>, grid, 512, L, s);
+    case 112: L.ntiles = tiles(1024 * 4); return launch(decim_stream2_cf32<127, 4, 1024, true, 4, true, 2, true, true, true, true>, grid, 1024, L, s);
+    case 113: L.ntiles = tiles(1024 * 4); return launch(decim_stream2_cf32<127, 4, 1024, true, 4, true, 0, true, true, true, true>, grid, 1024, L, s);
+    case 114: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 3, true, true, true, true>, grid, 512, L, s);
+    case 120: L.ntiles = tiles(256 * 8); return launch(decim_stream2_cf32<127, 8, 256, true, 2, true, 0, true, true, true, true>, grid, 256, L, s);
+    case 121: L.ntiles = tiles(256 * 8); return launch(decim_stream2_cf32<127, 8, 256, true, 2, true, 2, true, true, true, true>, grid, 256, L, s);
+    case 122: L.ntiles = tiles(512 * 8); return launch(decim_stream2_cf32<127, 8, 512, true, 2, true, 0, true, true, true, true>, grid, 512, L, s);
+    case 123: L.ntiles = tiles(128 * 8); return launch(decim_stream2_cf32<127, 8, 128, true, 2, true, 0, true, true, true, true>, grid, 128, L, s);
     case 24: L.ntiles = tiles(128 * 8); return launch(decim_stream2_cf32<127, 8, 128, true, 2, true>, grid, 128, L, s);
     default: return -1;
     }

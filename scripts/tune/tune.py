@@ -94,6 +94,15 @@ def main():
                     (80, 1024, "PROBE1 512 g1024"), (80, 512, "PROBE1 512 g512"), (90, 256, "PROBE1 512 mw2 g256"),
                     (84, 1024, "PROBE1 256 g1024"), (88, 1024, "256 lanes g1024"), (48, 1024, "head g1024 (again)"),
                     (-1, 1024, "previous head g1024 (again)")]
+    if os.environ.get("TUNE_COMPUTE"):  # PROBE2 = compute path only (L2-resident input)
+        variants = [(48, 1024, "head g1024"), (110, 1024, "PROBE2 512 mw4 g1024"), (114, 1024, "PROBE3 (no tap loads) g1024"),
+                    (110, 512, "PROBE2 512 mw4 g512"),
+                    (111, 256, "PROBE2 512 mw2 g256"), (112, 256, "PROBE2 1024 mw4 g256"),
+                    (113, 256, "1024 mw4 g256"), (90, 256, "PROBE1 512 mw2 g256"), (80, 1024, "PROBE1 512 g1024")]
+    if os.environ.get("TUNE_R8"):  # 8 outputs per lane (half the LDS reads per output), 2 waves/SIMD
+        variants = [(48, 1024, "head g1024"), (120, 512, "R8 256 g512"), (120, 1024, "R8 256 g1024"),
+                    (121, 512, "PROBE2 R8 256 g512"), (122, 256, "R8 512 g256"), (123, 1024, "R8 128 g1024"),
+                    (123, 2048, "R8 128 g2048"), (110, 1024, "PROBE2 head g1024"), (48, 1024, "head g1024 (again)")]
     if os.environ.get("TUNE_SUSTAINED_ONLY"):
         sustained_rounds(variants, x, y, cdev, h0, h1, stream, L, ref)
         return

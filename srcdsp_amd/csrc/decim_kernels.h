@@ -215,7 +215,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
     float4 v[PER];
     // tiles >= 1: one descriptor per tile, 32-bit lane offsets, range-checked
     auto stage_load = [&](float4 (&v)[PER], long tile) {
-        if constexpr (PROBE == 2) tile = 1 + (tile & 15);
+        if constexpr (PROBE >= 2) tile = 1 + (tile & 15);
         const long b0 = 4 * tile * TO - 4 * NQ;  // >= 0 for tile >= 1
         const long remb = (n_in - b0) * 8;
         const unsigned nrec = (unsigned)(remb > 0xfffffff0L ? 0xfffffff0L : (remb < 0 ? 0 : remb));
@@ -296,7 +296,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
             for (int p = 0; p < 4; ++p) {
                 const int k = 4 * q + p;
                 if (k < NT) {
-                    const float c = tp[k];
+                    // PROBE 3 (timing only): compute path with one tap value, no tap loads
+                    const float c = PROBE == 3 ? __builtin_bit_cast(float, a.shift | 0x3c000000u) : tp[k];
 #pragma unroll
                     for (int r = 0; r < R; ++r) {
                         const float2 x = X[4 * (r - q) - p + 4 * NQ];
