@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <string>
 
@@ -91,6 +92,15 @@ __device__ __forceinline__ ConstPtr<T> const_view(const void *p) {
 
 constexpr int floordiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
 constexpr int ceildiv(int a, int b) { return (a + b - 1) / b; }
+
+// ------------------------------------------------------------ host copies
+// host memcpy into / out of pinned staging buffers, split over a persistent
+// pool of host threads for large copies (one thread cannot fill the host link)
+void host_copy(void *dst, const void *src, size_t bytes);
+// fn(part, parts) on the caller and the pool's threads (runtime.hip)
+void host_parallel(const std::function<void(int, int)> &fn);
+void host_piece(size_t n, int part, int parts, size_t *lo, size_t *hi);
+int host_threads();
 
 // --------------------------------------------------------- host semantics
 // coeffScaling = static_cast<int>(floor(log2(sum |c|)))  (dnsampling_filters.h:92-95,

@@ -688,7 +688,7 @@ SRCDSP_API int srcdsp_corr_step_host(srcdsp_corr_t h, const void *in, size_t n, 
     srcdsp_corr_state &c = h->c;
     int rc = c.stage.reserve(4 * n, 4 * n);
     if (rc) return rc;
-    memcpy(c.stage.h_buf, in, 4 * n);
+    host_copy(c.stage.h_buf, in, 4 * n);
     SRCDSP_HIP_TRY(hipMemcpyAsync(c.stage.d_buf, c.stage.h_buf, 4 * n, hipMemcpyHostToDevice, c.stage.stream));
     return corr_run(c, (const uint32_t *)c.stage.d_buf, n, found, corr_index, c.stage.stream);
 }

@@ -355,13 +355,13 @@ static int core_step_host(FirCore &f, const void *in, size_t n_in, void *out, si
     if (rc) return rc;
     hipStream_t s = f.stage.stream;
     char *d_in = (char *)f.stage.d_buf, *d_out = d_in + ib_al;
-    memcpy(f.stage.h_buf, in, ib);
+    host_copy(f.stage.h_buf, in, ib);
     SRCDSP_HIP_TRY(hipMemcpyAsync(d_in, f.stage.h_buf, ib, hipMemcpyHostToDevice, s));
     rc = core_step(f, d_in, n_in, d_out, n_out, s, nullptr);
     if (rc) return rc;
     SRCDSP_HIP_TRY(hipMemcpyAsync(f.stage.h_buf, d_out, ob, hipMemcpyDeviceToHost, s));
     SRCDSP_HIP_TRY(hipStreamSynchronize(s));
-    memcpy(out, f.stage.h_buf, ob);
+    host_copy(out, f.stage.h_buf, ob);
     return SRCDSP_OK;
 }
 

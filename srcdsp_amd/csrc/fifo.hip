@@ -19,8 +19,12 @@
 // bytes, interleaved I,Q.  readBinarySamples (:250-262) is fixed as SURVEY 8f
 // asks: the output is cleared first (the reference calls out.empty()) and
 // only whole samples are returned (the reference's while(is) loop appends one
-// indeterminate sample at EOF).  Device loads overlap fread with H2D copies
-// through two pinned chunks.
+// indeterminate sample at EOF).  Device loads overlap a parallel pread of one
+// pinned chunk with the H2D copy of the other.
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <iostream>
@@ -195,7 +199,7 @@ SRCDSP_API int srcdsp_fifo_write(srcdsp_fifo_t h, const void *in, size_t n, unsi
         const size_t m = std::min(n - done, stage / f.es);
         const int k = f.k;
         if (f.pin_busy[k]) SRCDSP_HIP_TRY(hipEventSynchronize(f.ev_pin[k]));  // its previous copy has landed
-        memcpy(f.pin[k], src + done * f.es, m * f.es);
+        host_copy(f.pin[k], src + done * f.es, m * f.es);
         int rc = ring_put(f, (p + done) % f.N, (const char *)f.pin[k], m, hipMemcpyHostToDevice, f.cs);
         if (rc) return rc;
         SRCDSP_HIP_TRY(hipEventRecord(f.ev_pin[k], f.cs));
@@ -276,7 +280,7 @@ SRCDSP_API int srcdsp_fifo_read_host(srcdsp_fifo_t h, void *out, size_t n, uint6
     int rc = ring_get(f, sp, ep, (char *)f.h_rd, hipMemcpyDeviceToHost, f.cs);
     if (rc) return rc;
     SRCDSP_HIP_TRY(hipStreamSynchronize(f.cs));
-    memcpy(out, f.h_rd, n * f.es);
+    host_copy(out, f.h_rd, n * f.es);
     return SRCDSP_OK;
 }
 
@@ -385,7 +389,39 @@ SRCDSP_API int srcdsp_iq_load_host(const char *path, size_t component_bytes, voi
     return SRCDSP_OK;
 }
 
-// file -> device: fread of chunk i+1 overlaps the H2D copy of chunk i
+// Pinned staging of the capture loads, kept across calls (allocating 2 pinned
+// chunks per call cost more than the copy of a small capture); one load at a
+// time uses it.
+namespace {
+struct IqStage {
+    std::mutex mx;
+    void *pin[2] = {nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    size_t cap = 0;
+    int reserve(size_t bytes) {
+        if (cap >= bytes) return SRCDSP_OK;
+        for (int b = 0; b < 2; ++b) {
+            if (pin[b]) (void)hipHostFree(pin[b]);
+            pin[b] = nullptr;
+        }
+        cap = 0;
+        for (int b = 0; b < 2; ++b) {
+            SRCDSP_HIP_TRY(hipHostMalloc(&pin[b], bytes, hipHostMallocDefault));
+            if (!ev[b]) SRCDSP_HIP_TRY(hipEventCreateWithFlags(&ev[b], hipEventDisableTiming));
+        }
+        cap = bytes;
+        return SRCDSP_OK;
+    }
+};
+IqStage &iq_stage() {
+    static IqStage *s = new IqStage();  // lives until exit
+    return *s;
+}
+constexpr size_t kIqChunk = 32u << 20;
+}  // namespace
+
+// file -> device: the pread of chunk i+1 (split over the host pool's threads)
+// overlaps the H2D copy of chunk i
 SRCDSP_API int srcdsp_iq_load(const char *path, size_t component_bytes, void *d_out, size_t cap, size_t *n,
                               void *stream) {
     int rc = srcdsp_iq_count(path, component_bytes, n);
@@ -397,36 +433,48 @@ SRCDSP_API int srcdsp_iq_load(const char *path, size_t component_bytes, void *d_
     }
     const size_t bytes = *n * 2 * component_bytes;
     if (bytes == 0) return SRCDSP_OK;
-    FILE *fp = open_or_err(path, "rb");
-    if (!fp) return SRCDSP_ERR_ARG;
+    const int fd = ::open(path, O_RDONLY);
+    if (fd < 0) {
+        set_error(std::string("cannot open ") + path);
+        return SRCDSP_ERR_ARG;
+    }
     hipStream_t s = (hipStream_t)stream;
-    void *pin[2] = {nullptr, nullptr};
-    hipEvent_t ev[2] = {nullptr, nullptr};
-    const size_t chunk = std::min(kStageBytes, bytes);
-    int err = SRCDSP_OK;
-    for (int b = 0; b < 2 && !err; ++b)
-        if (hipHostMalloc(&pin[b], chunk, hipHostMallocDefault) != hipSuccess ||
-            hipEventCreateWithFlags(&ev[b], hipEventDisableTiming) != hipSuccess)
-            err = SRCDSP_ERR_HIP;
+    IqStage &st = iq_stage();
+    std::lock_guard<std::mutex> lock(st.mx);
+    const size_t chunk = std::min(kIqChunk, bytes);
+    int err = st.reserve(chunk);
     bool used[2] = {false, false};
     for (size_t done = 0, k = 0; !err && done < bytes; done += chunk, k ^= 1) {
         const size_t m = std::min(chunk, bytes - done);
-        if (used[k] && hipEventSynchronize(ev[k]) != hipSuccess) err = SRCDSP_ERR_HIP;
-        if (!err && std::fread(pin[k], 1, m, fp) != m) {
+        if (used[k] && hipEventSynchronize(st.ev[k]) != hipSuccess) err = SRCDSP_ERR_HIP;
+        if (err) break;
+        std::atomic<bool> short_read{false};
+        char *dst = (char *)st.pin[k];
+        host_parallel([&](int part, int parts) {
+            size_t lo, hi;
+            host_piece(m, part, parts, &lo, &hi);
+            while (lo < hi) {
+                const ssize_t r = ::pread(fd, dst + lo, hi - lo, (off_t)(done + lo));
+                if (r <= 0) {
+                    short_read = true;
+                    return;
+                }
+                lo += (size_t)r;
+            }
+        });
+        if (short_read) {
             set_error("iq_load: short read");
             err = SRCDSP_ERR_ARG;
         }
-        if (!err && (hipMemcpyAsync((char *)d_out + done, pin[k], m, hipMemcpyHostToDevice, s) != hipSuccess ||
-                     hipEventRecord(ev[k], s) != hipSuccess))
+        if (!err && (hipMemcpyAsync((char *)d_out + done, st.pin[k], m, hipMemcpyHostToDevice, s) != hipSuccess ||
+                     hipEventRecord(st.ev[k], s) != hipSuccess))
             err = SRCDSP_ERR_HIP;
         used[k] = true;
     }
-    if (hipStreamSynchronize(s) != hipSuccess && !err) err = SRCDSP_ERR_HIP;
-    std::fclose(fp);
-    for (int b = 0; b < 2; ++b) {
-        if (pin[b]) (void)hipHostFree(pin[b]);
-        if (ev[b]) (void)hipEventDestroy(ev[b]);
-    }
+    // the staging is reused by the next load: its copies must have landed
+    for (int b = 0; b < 2; ++b)
+        if (used[b] && hipEventSynchronize(st.ev[b]) != hipSuccess && !err) err = SRCDSP_ERR_HIP;
+    ::close(fd);
     if (err == SRCDSP_ERR_HIP) set_error("iq_load: HIP staging failed");
     return err;
 }

@@ -228,13 +228,13 @@ SRCDSP_API int srcdsp_mixer_step_host(srcdsp_mixer_t h, const void *in, size_t n
     if (rc) return rc;
     hipStream_t s = m.stage.stream;
     char *d_in = (char *)m.stage.d_buf, *d_out = d_in + bal;
-    memcpy(m.stage.h_buf, in, b);
+    host_copy(m.stage.h_buf, in, b);
     SRCDSP_HIP_TRY(hipMemcpyAsync(d_in, m.stage.h_buf, b, hipMemcpyHostToDevice, s));
     rc = mixer_launch(m, d_in, n, d_out, s);
     if (rc) return rc;
     SRCDSP_HIP_TRY(hipMemcpyAsync(m.stage.h_buf, d_out, b, hipMemcpyDeviceToHost, s));
     SRCDSP_HIP_TRY(hipStreamSynchronize(s));
-    memcpy(out, m.stage.h_buf, b);
+    host_copy(out, m.stage.h_buf, b);
     return SRCDSP_OK;
 }
 

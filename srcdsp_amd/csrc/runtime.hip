@@ -4,13 +4,108 @@
 // sample generator used by benchmarks.
 #include "common.h"
 
+#include <algorithm>
+#include <condition_variable>
 #include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <thread>
 
 namespace srcdsp {
 
 static thread_local std::string g_err;
 void set_error(const std::string &m) { g_err = m; }
 const char *get_error() { return g_err.c_str(); }
+
+// ------------------------------------------------------------ host copies
+// host_parallel(fn): fn(part, parts) on the caller and parts-1 pool threads,
+// returns when all are done.  The staging copies and capture reads use it to
+// cut one large transfer into `parts` cache-line-aligned pieces (one host
+// thread cannot fill the host link).  parts = SRCDSP_HOST_COPY_THREADS
+// (default 8), capped by the machine.  Calls from different caller threads
+// are serialized (one pool).  The pool is created on first use and lives until
+// exit (detached threads parked on a condvar).
+namespace {
+class HostPool {
+  public:
+    static HostPool &get() {
+        static HostPool *p = new HostPool();
+        return *p;
+    }
+    int threads() const { return T; }
+    void run(const std::function<void(int, int)> &fn) {
+        std::lock_guard<std::mutex> call(call_mx);
+        {
+            std::lock_guard<std::mutex> g(mx);
+            job = &fn;
+            remaining = T - 1;
+            ++gen;
+        }
+        cv_work.notify_all();
+        fn(0, T);
+        std::unique_lock<std::mutex> g(mx);
+        cv_done.wait(g, [&] { return remaining == 0; });
+    }
+
+  private:
+    HostPool() {
+        const char *e = std::getenv("SRCDSP_HOST_COPY_THREADS");
+        int want = e ? std::atoi(e) : 8;
+        const int hw = (int)std::thread::hardware_concurrency();
+        T = std::max(1, std::min(want, hw > 0 ? hw : 1));
+        for (int i = 1; i < T; ++i) std::thread([this, i] { worker(i); }).detach();
+    }
+    void worker(int id) {
+        unsigned seen = 0;
+        for (;;) {
+            const std::function<void(int, int)> *fn;
+            {
+                std::unique_lock<std::mutex> g(mx);
+                cv_work.wait(g, [&] { return gen != seen; });
+                seen = gen;
+                fn = job;
+            }
+            (*fn)(id, T);
+            std::lock_guard<std::mutex> g(mx);
+            if (--remaining == 0) cv_done.notify_one();
+        }
+    }
+    int T = 1;
+    std::mutex call_mx, mx;
+    std::condition_variable cv_work, cv_done;
+    const std::function<void(int, int)> *job = nullptr;
+    unsigned gen = 0;
+    int remaining = 0;
+};
+constexpr size_t kParMin = 2u << 20;
+}  // namespace
+
+int host_threads() { return HostPool::get().threads(); }
+
+void host_parallel(const std::function<void(int, int)> &fn) {
+    if (HostPool::get().threads() == 1) return fn(0, 1);
+    HostPool::get().run(fn);
+}
+
+// [lo, hi) of piece `part` of `parts` over n bytes, 64-B aligned cuts
+void host_piece(size_t n, int part, int parts, size_t *lo, size_t *hi) {
+    const size_t step = (n / (size_t)parts + 63) & ~(size_t)63;
+    *lo = std::min(n, step * (size_t)part);
+    *hi = part == parts - 1 ? n : std::min(n, *lo + step);
+}
+
+void host_copy(void *dst, const void *src, size_t bytes) {
+    if (bytes < kParMin || HostPool::get().threads() == 1) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    host_parallel([&](int part, int parts) {
+        size_t lo, hi;
+        host_piece(bytes, part, parts, &lo, &hi);
+        if (hi > lo) std::memcpy((char *)dst + lo, (const char *)src + lo, hi - lo);
+    });
+}
 
 int32_t cvt_d2i_x86(double d) {
     if (!(d > -2147483649.0 && d < 2147483648.0)) return INT32_MIN;

@@ -583,7 +583,7 @@ SRCDSP_API int srcdsp_up_step_host(srcdsp_up_t h, const void *in, size_t n_in, v
     hipStream_t s = u.stage.stream;
     char *d_in = (char *)u.stage.d_buf, *d_out = d_in + ib_al;
     if (ib) {
-        memcpy(u.stage.h_buf, in, ib);
+        host_copy(u.stage.h_buf, in, ib);
         SRCDSP_HIP_TRY(hipMemcpyAsync(d_in, u.stage.h_buf, ib, hipMemcpyHostToDevice, s));
     }
     rc = up_launch(u, d_in, n_in, d_out, n_out, flush != 0, iterator != 0, s);
@@ -593,7 +593,7 @@ SRCDSP_API int srcdsp_up_step_host(srcdsp_up_t h, const void *in, size_t n_in, v
     const size_t wb = std::min(ob, (size_t)u.L * (n_in + (flush ? u.length / u.L : 0)) * eb);
     SRCDSP_HIP_TRY(hipMemcpyAsync(u.stage.h_buf, d_out, wb, hipMemcpyDeviceToHost, s));
     SRCDSP_HIP_TRY(hipStreamSynchronize(s));
-    memcpy(out, u.stage.h_buf, wb);
+    host_copy(out, u.stage.h_buf, wb);
     return SRCDSP_OK;
 }
 
