@@ -12,6 +12,7 @@
 #include <functional>
 #include <mutex>
 #include <string>
+#include <type_traits>
 
 #include "../../include/srcdsp_hip.h"
 

@@ -266,8 +266,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
     // issues the next tile's loads before this and lands them in LDS after
     // it, all in one iteration: the compiler then waits for the loads with
     // vmcnt(this tile's stores) and the stores stay in flight.
-    auto do_tile = [&](long tile) {
-
+    // WHOLE: the tile's TO outputs all exist (every tile but a partial last one)
+    auto do_tile = [&](long tile, auto whole_tag) {
+        constexpr bool WHOLE = decltype(whole_tag)::value;
         ConstPtr<float> tp = const_view<float>(a.coef);
         asm volatile("" : "+s"(tp));
         float2 X[4 * (NQ + R)];
@@ -320,7 +321,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
             for (int r = 0; r < R; ++r) ob[t * R + r] = make_float2(q(yr[r]), q(yi[r]));
             SRCDSP_LDS_BARRIER();
             const float4 *ob4 = (const float4 *)lds;
-            if (o0 + TO <= a.n_out) {
+            if constexpr (WHOLE) {
 #pragma unroll
                 for (int i = 0; i < TO / 2 / BLOCK; ++i) {
                     const int k = t + i * BLOCK;
@@ -340,7 +341,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
                 for (int k = t; k < TO; k += BLOCK)
                     if (o0 + k < a.n_out) out[o0 + k] = ob[k];
             }
-        } else if (n0 + R <= a.n_out && (R % 2) == 0) {
+        } else if (WHOLE && (R % 2) == 0) {
 #pragma unroll
             for (int r = 0; r < R; r += 2)
                 store16<NTS>((float4 *)(out + n0 + r), make_float4(q(yr[r]), q(yi[r]), q(yr[r + 1]), q(yi[r + 1])));
@@ -350,13 +351,23 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
                 if (n0 + r < a.n_out) out[n0 + r] = make_float2(q(yr[r]), q(yi[r]));
         }
         };
-    if (t_begin < t_end) stage_to_lds();
-    for (long tile = t_begin; tile < t_end;) {
-        const long nxt = tile + t_step;
-        if (nxt < t_end) stage_load(v, nxt);
-        do_tile(tile);
-        if (nxt < t_end) stage_to_lds();
-        tile = nxt;
+    // Every iteration of the loop prefetches (the workgroup's last tile is
+    // peeled off after it), and only the launch's last tile can be partial, so
+    // the loop body is one straight path with a fixed number of stores: the
+    // compiler waits for the prefetch with a counted vmcnt and the stores stay
+    // in flight across iterations.
+    if (t_begin < t_end) {
+        stage_to_lds();
+        long tile = t_begin;
+        for (; tile + t_step < t_end; tile += t_step) {
+            stage_load(v, tile + t_step);
+            do_tile(tile, std::true_type{});
+            stage_to_lds();
+        }
+        if ((tile + 1) * TO <= a.n_out)
+            do_tile(tile, std::true_type{});
+        else
+            do_tile(tile, std::false_type{});
     }
 
 }
@@ -1018,7 +1029,8 @@ __global__ __launch_bounds__(kFirBlock, 4) void fir_stream_f32(DecimLaunch a) {
         for (int i = 0; i < PER; ++i) {
             const int g = t + i * BLOCK;
             if (g < TG) {
-                auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * g, 0, 2);  // aux 2 = nt
+                // lane offset in the VGPR, per-load step in soffset; aux 2 = nt
+                auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * t, 16 * i * BLOCK, 2);
                 v[i] = make_float4(__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]),
                                    __uint_as_float(w[3]));
             }
@@ -1042,7 +1054,9 @@ __global__ __launch_bounds__(kFirBlock, 4) void fir_stream_f32(DecimLaunch a) {
         }
     }
     ConstPtr<float> tp = const_view<float>(a.coef);
-    for (long tile = b; tile < a.ntiles; tile += nb) {
+    // the staged tile lands in LDS once every wave is done with the previous
+    // tile's image and output staging
+    auto stage_to_lds = [&]() {
         SRCDSP_LDS_BARRIER();
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
@@ -1050,7 +1064,12 @@ __global__ __launch_bounds__(kFirBlock, 4) void fir_stream_f32(DecimLaunch a) {
             if (g < TG) fl[slot(g)] = v[i];
         }
         SRCDSP_LDS_BARRIER();
-        if (tile + nb < a.ntiles) stage_load(tile + nb);
+    };
+    // as decim_stream2_cf32: the next tile's loads are issued before this
+    // tile's taps and land after its stores, in one iteration, so the wait
+    // for them leaves the stores in flight
+    auto do_tile = [&](long tile, auto whole_tag) {
+        constexpr bool WHOLE = decltype(whole_tag)::value;
         float2 o[R];
         fir_lane<KV, FMA>(fl, (P0 + R * t) / SPG, N, tp, a.shift, o);
         const long o0 = tile * TO;
@@ -1059,7 +1078,7 @@ __global__ __launch_bounds__(kFirBlock, 4) void fir_stream_f32(DecimLaunch a) {
 #pragma unroll
         for (int r = 0; r < R; ++r) ob[t * R + r] = o[r];
         SRCDSP_LDS_BARRIER();
-        if (o0 + TO <= a.n_out) {
+        if constexpr (WHOLE) {
 #pragma unroll
             for (int i = 0; i < LOUT / BLOCK; ++i) {
                 const int k = t + i * BLOCK;
@@ -1069,6 +1088,20 @@ __global__ __launch_bounds__(kFirBlock, 4) void fir_stream_f32(DecimLaunch a) {
             for (int k = t; k < TO; k += BLOCK)
                 if (o0 + k < a.n_out) out[o0 + k] = ob[k];
         }
+    };
+    // prefetching loop, the workgroup's last tile peeled (as decim_stream2_cf32)
+    if (b < a.ntiles) {
+        stage_to_lds();
+        long tile = b;
+        for (; tile + nb < a.ntiles; tile += nb) {
+            stage_load(tile + nb);
+            do_tile(tile, std::true_type{});
+            stage_to_lds();
+        }
+        if ((tile + 1) * TO <= a.n_out)
+            do_tile(tile, std::true_type{});
+        else
+            do_tile(tile, std::false_type{});
     }
 }
 
