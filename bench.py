@@ -5,13 +5,15 @@ Default workload = BASELINE.json configs[1] (the headline metric): the 127-tap
 complex<float> decimate-by-4 FilterDnsamplingFir over 2^28 device-resident
 synthetic samples, one step() per timed step (one kernel launch), FMA float
 contract.  With --gpus N (launched by torch.distributed.run) every rank owns
-its own channel(s) -- configs[2]'s channel sharding, weak scaling, no
+8 channels (default at N>1; --channels-per-gpu) -- configs[2]'s 64 channels
+over 8 GPUs, one batched launch per step per rank, weak scaling, no
 collective in the timed region; the RCCL result gather to rank 0 is timed
 separately (gather_ms).
 
 Other workloads (--workload): mixdecim (config 4, mixer -> fixed-point
 decimator, fused), corr (config 5, 1024-lag correlator), fir (config 1 shape on
-the GPU).
+the GPU), up (interpolator), fifo / iq (host -> HBM ring or capture replay
+feeding config 4's chain; bound by the host link).
 
 Reported beside the GPU number:
   roofline      dominant kernel's algorithmic bytes / its HIP-event time, vs 8 TB/s
@@ -48,7 +50,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=100)
     p.add_argument("--workload", default="decim", choices=["decim", "mixdecim", "corr", "fir", "up", "fifo", "iq"])
     p.add_argument("--samples", type=int, default=1 << 28, help="input samples per channel per step")
-    p.add_argument("--channels-per-gpu", type=int, default=1)
+    # default: 1 channel at N=1 (configs[1], the headline); 8 per GPU at N>1,
+    # i.e. configs[2]'s 64 independent channels over 8 GPUs, weak-scaled
+    p.add_argument("--channels-per-gpu", type=int, default=None)
     p.add_argument("--fp", default="fma", choices=["fma", "strict"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=1 << 27, help="samples timed on the reference CPU path")
@@ -456,6 +460,8 @@ def main():
     from srcdsp_amd.dist import gather_to_root, max_over_ranks
     S.lib()  # loud failure if the HIP library is missing
     L = args.samples - args.samples % 4
+    if args.channels_per_gpu is None:
+        args.channels_per_gpu = 1 if world == 1 or args.workload != "decim" else 8
     work = WORKLOADS[args.workload](S, torch, L, args.channels_per_gpu, rank, args.fp)
     stream = torch.cuda.current_stream()
 

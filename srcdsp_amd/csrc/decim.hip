@@ -134,6 +134,7 @@ int launch_fir_tile(const DecimLaunch &L0, int channels, bool fma, hipStream_t s
     DecimLaunch L = L0;
     L.ntiles = (L.n_out + TO - 1) / TO;
     if (L.ntaps <= kFirStreamTaps) {  // persistent, prefetching
+        // grid 512..2048 measure alike (0.650-0.660 ms, 2^28 samples, 31 taps); 256 is 1.7x slower
         dim3 grid((unsigned)std::min<long>(L.ntiles, kCfGridCap), channels);
         if (fma)
             hipLaunchKernelGGL((fir_stream_f32<KV, true>), grid, dim3(kFirBlock), 0, s, L);
