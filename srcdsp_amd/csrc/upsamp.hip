@@ -217,7 +217,7 @@ __global__ __launch_bounds__(kUpBlock) void up_tile(const uint32_t *in, long n_i
 // exactly the reference's complex<int32_t> arithmetic.
 constexpr int kUpRD = 8, kUpBlockD = 256;
 
-template <int LR>
+template <int LR, bool NTS = false>
 __global__ __launch_bounds__(kUpBlockD) void up_tile_dot2(const uint32_t *in, long n_in, long n_total,
                                                          const uint32_t *hist_in, uint32_t *hist_out,
                                                          const uint32_t *pairs, int H, unsigned shift, uint32_t *out) {
@@ -336,7 +336,12 @@ __global__ __launch_bounds__(kUpBlockD) void up_tile_dot2(const uint32_t *in, lo
         const uint4 v = ob[(G / GPLo) * STR + (G % GPLo)];
         const long w0 = wbase + 4L * G;
         if (w0 + 4 <= wend) {
-            *(uint4 *)(out + w0) = v;
+            if constexpr (NTS) {  // streaming store: the output is written once, 4L x the input bytes
+                typedef unsigned u4_t __attribute__((ext_vector_type(4)));
+                __builtin_nontemporal_store((u4_t){v.x, v.y, v.z, v.w}, (u4_t *)(out + w0));
+            } else {
+                *(uint4 *)(out + w0) = v;
+            }
         } else {
             const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
             for (int u = 0; u < 4; ++u)
@@ -436,14 +441,15 @@ static int up_launch(srcdsp_up_state &u, const void *d_in, size_t n_in, void *d_
         const size_t out_lds = 16 * (size_t)kUpBlockD * (kUpRD * u.L / 4 + 1);  // staged output tile
         const size_t smem = std::max(4 * 16 * (size_t)PGR, out_lds);
         const dim3 grid((unsigned)((n_total + TI - 1) / TI));
+        // non-temporal output stores: 0.414 -> 0.385 ms at L = 4, 128 taps, 2^26 inputs
+#define SRCDSP_UP_DOT2(LR)                                                                                        \
+    hipLaunchKernelGGL((up_tile_dot2<LR, true>), grid, dim3(kUpBlockD), smem, s, (const uint32_t *)d_in, (long)n_in, \
+                       n_total, (const uint32_t *)hin0, (uint32_t *)hout0, u.d_pair, u.H, shift, (uint32_t *)d_out)
         if (u.L == 2)
-            hipLaunchKernelGGL((up_tile_dot2<2>), grid, dim3(kUpBlockD), smem, s, (const uint32_t *)d_in, (long)n_in,
-                               n_total, (const uint32_t *)hin0, (uint32_t *)hout0, u.d_pair, u.H, shift,
-                               (uint32_t *)d_out);
+            SRCDSP_UP_DOT2(2);
         else
-            hipLaunchKernelGGL((up_tile_dot2<4>), grid, dim3(kUpBlockD), smem, s, (const uint32_t *)d_in, (long)n_in,
-                               n_total, (const uint32_t *)hin0, (uint32_t *)hout0, u.d_pair, u.H, shift,
-                               (uint32_t *)d_out);
+            SRCDSP_UP_DOT2(4);
+#undef SRCDSP_UP_DOT2
         SRCDSP_HIP_TRY(hipGetLastError());
         u.cur ^= 1;
         return u.order.after(s);
