@@ -155,7 +155,32 @@ extern "C" int tune_decim(int variant, int grid, const float *d_coef, const void
     case 121: L.ntiles = tiles(256 * 8); return launch(decim_stream2_cf32<127, 8, 256, true, 2, true, 2, true, true, true, true>, grid, 256, L, s);
     case 122: L.ntiles = tiles(512 * 8); return launch(decim_stream2_cf32<127, 8, 512, true, 2, true, 0, true, true, true, true>, grid, 512, L, s);
     case 123: L.ntiles = tiles(128 * 8); return launch(decim_stream2_cf32<127, 8, 128, true, 2, true, 0, true, true, true, true>, grid, 128, L, s);
+    // OST 2: permlane32-paired whole-line stores (no LDS output staging, 2 barriers per tile)
+    case 70: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, 2, true, true>, grid, 512, L, s);
+    case 71: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 1, true, 2, true, true>, grid, 512, L, s);
+    case 72: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 2, true, 0, true, 2, true, true>, grid, 512, L, s);
+    case 73: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 2, true, 2, true, true>, grid, 512, L, s);
+    case 74: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 0, true, 2, true, true>, grid, 256, L, s);
+    case 75: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, 0, true, true>, grid, 512, L, s);
     case 24: L.ntiles = tiles(128 * 8); return launch(decim_stream2_cf32<127, 8, 128, true, 2, true>, grid, 128, L, s);
     default: return -1;
     }
+}
+
+// ---- FilterFir stream kernel (float in, 31 taps): output store shapes
+extern "C" int tune_fir(int variant, int grid, const float *d_coef, const void *in, void *out, long n_in, int ntaps,
+                        unsigned shift, const void *hist_in, void *hist_out, void *stream) {
+    DecimLaunch L{};
+    L.in = in; L.out = out; L.n_in = n_in; L.n_out = n_in; L.ntaps = ntaps; L.shift = shift;
+    L.hist_in[0] = hist_in; L.hist_out[0] = hist_out;
+    L.coef = d_coef;
+    L.ntiles = (L.n_out + kFirR * kFirBlock - 1) / (kFirR * kFirBlock);
+    hipStream_t s = (hipStream_t)stream;
+    switch (variant) {
+    case 0: return launch(fir_stream_f32<KV_F32_REAL, true, 1>, grid, kFirBlock, L, s);
+    case 1: return launch(fir_stream_f32<KV_F32_REAL, true, 2>, grid, kFirBlock, L, s);
+    case 2: return launch(fir_stream_f32<KV_CF32, true, 1>, grid, kFirBlock, L, s);
+    case 3: return launch(fir_stream_f32<KV_CF32, true, 2>, grid, kFirBlock, L, s);
+    }
+    return -1;
 }

@@ -103,6 +103,15 @@ def main():
         variants = [(48, 1024, "head g1024"), (120, 512, "R8 256 g512"), (120, 1024, "R8 256 g1024"),
                     (121, 512, "PROBE2 R8 256 g512"), (122, 256, "R8 512 g256"), (123, 1024, "R8 128 g1024"),
                     (123, 2048, "R8 128 g2048"), (110, 1024, "PROBE2 head g1024"), (48, 1024, "head g1024 (again)")]
+    if os.environ.get("TUNE_OST"):  # output store shapes: LDS staging (product) vs permlane32 pairing vs none
+        variants = [(48, 1024, "head g1024"), (70, 1024, "OST2 g1024"), (70, 512, "OST2 g512"),
+                    (72, 256, "OST2 mw2 g256"), (72, 512, "OST2 mw2 g512"), (74, 1024, "OST2 256 g1024"),
+                    (74, 2048, "OST2 256 g2048"), (75, 1024, "OST0 g1024"),
+                    (71, 1024, "PROBE1 OST2 g1024"), (73, 1024, "PROBE2 OST2 g1024"), (110, 1024, "PROBE2 head g1024"),
+                    (48, 1024, "head g1024 (again)"), (70, 1024, "OST2 g1024 (again)")]
+    if os.environ.get("TUNE_FIR"):
+        fir_ab()
+        return
     if os.environ.get("TUNE_SUSTAINED_ONLY"):
         sustained_rounds(variants, x, y, cdev, h0, h1, stream, L, ref)
         return
@@ -128,6 +137,62 @@ def main():
         print(f"  {v[2]:28s} {res[v][0]:8s} {tmin:.4f} ms  {L / tmin / 1e6:8.1f} Gsamp/s  {gbs:7.1f} GB/s "
               f"({gbs / 8000 * 100:.1f}% of 8 TB/s)")
     sustained(variants, x, y, cdev, h0, h1, stream, L)
+
+
+def fir_ab(rounds=4, reps=30):
+    """FilterFir stream kernel (31 taps, 2^28 samples): LDS-staged vs lane-transposed output stores."""
+    lib.tune_fir.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_long, C.c_int, C.c_uint,
+                             C.c_void_p, C.c_void_p, C.c_void_p]
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    L = 1 << 28
+    c = hamming_sinc(31, 0.2)
+    cdev = torch.from_numpy(c.astype(np.float32)).cuda()
+    h0 = torch.zeros(64, dtype=torch.complex64, device="cuda")
+    h1 = torch.zeros(64, dtype=torch.complex64, device="cuda")
+    cases = []
+    for kin, var0 in (("float", 0), ("complex<float>", 2)):
+        if kin == "float":
+            x = torch.randint(-2048, 2048, (L,), device="cuda").float()
+        else:
+            x = torch.randint(-2048, 2048, (L, 2), device="cuda").float().view(torch.complex64).view(-1)
+        ref = S.FilterFir(c, kin, "complex<float>", kin, "float").step(x)
+        y = torch.empty(L, dtype=torch.complex64, device="cuda")
+        shift = None
+        for sh in range(0, 8):
+            y.zero_()
+            lib.tune_fir(var0, 2048, cdev.data_ptr(), x.data_ptr(), y.data_ptr(), L, 31, sh, h0.data_ptr(),
+                         h1.data_ptr(), stream)
+            torch.cuda.synchronize()
+            if torch.equal(y.view(torch.int32), ref.view(torch.int32)):
+                shift = sh
+                break
+        assert shift is not None, "no shift reproduces the product FIR"
+        for v in (var0, var0 + 1):
+            y.zero_()
+            lib.tune_fir(v, 2048, cdev.data_ptr(), x.data_ptr(), y.data_ptr(), L, 31, shift, h0.data_ptr(),
+                         h1.data_ptr(), stream)
+            torch.cuda.synchronize()
+            assert torch.equal(y.view(torch.int32), ref.view(torch.int32)), (kin, v)
+            cases.append((kin, v, x, y, shift))
+    st = torch.cuda.current_stream()
+    res = {(k, v): [] for k, v, *_ in cases}
+    for rnd in range(rounds):
+        for kin, v, x, y, shift in cases:
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+            for i in range(reps):
+                ev[i][0].record(st)
+                lib.tune_fir(v, 2048, cdev.data_ptr(), x.data_ptr(), y.data_ptr(), L, 31, shift, h0.data_ptr(),
+                             h1.data_ptr(), stream)
+                ev[i][1].record(st)
+            torch.cuda.synchronize()
+            res[(kin, v)].append(float(np.median([a.elapsed_time(b) for a, b in ev][-20:])))
+    print("FilterFir stream kernel, 31 taps, 2^28 samples (bit-exact vs the product checked); "
+          f"{rounds} interleaved rounds x {reps} launches, median of last 20:")
+    for (kin, v), r in res.items():
+        bps = 12 if kin == "float" else 16
+        print(f"  {kin:15s} {'LDS-staged stores' if v % 2 == 0 else 'lane-transposed stores':24s} "
+              f"min {min(r):.4f} median {np.median(r):.4f} ms -> {bps * L / (np.median(r) * 1e-3) / 1e9:7.1f} GB/s "
+              f"rounds {' '.join(f'{t:.4f}' for t in r)}", flush=True)
 
 
 def sustained_rounds(variants, x, y, cdev, h0, h1, stream, L, ref, rounds=4, reps=30):

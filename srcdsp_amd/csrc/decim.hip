@@ -16,8 +16,9 @@
 //    tile's FMA work.  Each lane owns R consecutive outputs and walks the taps
 //    as 4 polyphase register windows that slide one sample per 4 taps; taps
 //    are wave-uniform SGPR operands; each output is ONE sequential fma chain
-//    in ascending k (FMA) or separately rounded mul+add (!FMA).  Outputs go
-//    back through LDS into whole-line non-temporal stores.
+//    in ascending k (FMA) or separately rounded mul+add (!FMA).  Outputs are
+//    paired across the two half-waves (v_permlane32_swap) so each store
+//    instruction writes 1 KiB of whole lines, non-temporal.
 //  * decim_dot2_ci16<NT,BLOCK,MIX,MINW,TAB2> -- complex<int16_t> x int16-range
 //    taps on v_dot2 tap pairs over planar int16 LDS images, optionally with
 //    the NCO mixer of mixers.h fused into the staging pass (config 4).
@@ -64,10 +65,11 @@ int launch_cf32(DecimLaunch L, int channels, bool fma, hipStream_t s) {
     const bool q0 = (L.shift & 31u) == 0;  // limitScale16 shift 0: the 4-op float quantiser
     // measured best (scripts/tune, sustained back-to-back): 512-lane tiles
     // (8192 samples: half the halo re-read of 256), grid-stride tile order,
-    // non-temporal input loads, outputs staged through LDS into whole-line
-    // non-temporal stores; 2 workgroups (16 waves) per CU
+    // non-temporal input loads, outputs paired across half-waves by
+    // v_permlane32_swap into whole-line non-temporal stores (no LDS round
+    // trip: 2 barriers per tile, not 4); 2 workgroups (16 waves) per CU
 #define SRCDSP_CF32(F, Q) \
-    hipLaunchKernelGGL((decim_stream2_cf32<NT, kCfR, kCfBlock, F, 4, Q, 0, true, true, true, true>), grid, \
+    hipLaunchKernelGGL((decim_stream2_cf32<NT, kCfR, kCfBlock, F, 4, Q, 0, true, 2, true, true>), grid, \
                        dim3(kCfBlock), 0, s, L)
     if (fma && q0)
         SRCDSP_CF32(true, true);

@@ -182,9 +182,63 @@ __device__ __forceinline__ void store16(float4 *p, float4 v) {
         *p = v;
     }
 }
-template <int NT, int R, int BLOCK, bool FMA, int MINW, bool Q0, int PROBE = 0, bool NTL = false, bool OST = false,
+// Whole-line stores of one wave's outputs without an LDS round trip.  Lane l
+// holds R = 4 or 8 consecutive float2 outputs (wave output l*R + r), i.e.
+// R/2 16-B units; storing them as they stand would make every store
+// instruction half- or quarter-cover its 128-B lines.  A transpose of units
+// across 32-lane halves (v_permlane32_swap) and, for R = 8, 16-lane rows
+// (v_permlane16_swap) leaves in register j the units of lanes
+// [64j/(R/2), 64(j+1)/(R/2)): each store instruction then writes 1 KiB of
+// whole lines.  wo = the wave's first output; ln = lane in wave.
+template <int R, bool NTS>
+__device__ __forceinline__ void store_wave_lines(float2 *wo, const float2 (&o)[R], int ln) {
+    static_assert(R == 4 || R == 8, "4 or 8 outputs per lane");
+    constexpr int U = R / 2;  // 16-B units per lane
+    unsigned u[U][4];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+        u[k][0] = __float_as_uint(o[2 * k].x);
+        u[k][1] = __float_as_uint(o[2 * k].y);
+        u[k][2] = __float_as_uint(o[2 * k + 1].x);
+        u[k][3] = __float_as_uint(o[2 * k + 1].y);
+    }
+    // vdst rows of the upper half <-> vsrc rows of the lower half
+#pragma unroll
+    for (int k = 0; k < U / 2; ++k)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            auto sw = __builtin_amdgcn_permlane32_swap(u[k][d], u[k + U / 2][d], false, false);
+            u[k][d] = sw[0];
+            u[k + U / 2][d] = sw[1];
+        }
+    if constexpr (U == 4) {  // odd 16-lane rows of vdst <-> even rows of vsrc
+#pragma unroll
+        for (int k = 0; k < U; k += 2)
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                auto sw = __builtin_amdgcn_permlane16_swap(u[k][d], u[k + 1][d], false, false);
+                u[k][d] = sw[0];
+                u[k + 1][d] = sw[1];
+            }
+    }
+    // register j, lane ln: unit (ln / (64/U)) of lane (64/U) j + ln % (64/U)
+    constexpr int LPJ = 64 / U;
+    float2 *base = wo + (ln % LPJ) * R + 2 * (ln / LPJ);
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+        store16<NTS>((float4 *)(base + LPJ * R * j), make_float4(__uint_as_float(u[j][0]), __uint_as_float(u[j][1]),
+                                                                __uint_as_float(u[j][2]), __uint_as_float(u[j][3])));
+}
+// OST: 0 = each lane stores its own R outputs (two 16-B stores at a 32-B lane
+// stride: every store instruction half-covers its lines); 1 = outputs staged
+// through LDS (two barriers per tile); 2 (R == 4 only) = a v_permlane32_swap
+// per dword pairs lane i's first output pair with lane i+32's and lane i+32's
+// second pair with lane i's, so each of the two store instructions writes
+// 1 KiB of whole lines, with no LDS round trip and no barrier.
+template <int NT, int R, int BLOCK, bool FMA, int MINW, bool Q0, int PROBE = 0, bool NTL = false, int OST = 0,
           bool NTS = false, bool GS = false, int LAUX = -1, int SAUX = -1>
 __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a) {
+    static_assert(OST != 2 || R == 4, "the permlane32 store pairing assumes 4 outputs per lane");
     constexpr int NQ = (NT + 3) / 4;
     constexpr int TO = BLOCK * R;
     constexpr int TG = 2 * TO + 2 * NQ;
@@ -311,7 +365,16 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
         const long n0 = tile * TO + (long)t * R;
         const unsigned sh = a.shift;
         auto q = [&](float y) { return Q0 ? q16f_shift0(y) : q16f(y, sh); };
-        if constexpr (OST) {
+        if constexpr (OST == 2 && WHOLE) {
+            float2 o[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) o[r] = make_float2(q(yr[r]), q(yi[r]));
+            store_wave_lines<R, NTS>(out + tile * TO + (t & ~63) * R, o, t & 63);
+        } else if constexpr (OST == 2) {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (n0 + r < a.n_out) out[n0 + r] = make_float2(q(yr[r]), q(yi[r]));
+        } else if constexpr (OST == 1) {
             // outputs -> LDS (reusing the tile image once every wave is done
             // reading it) -> 16-B lane-contiguous stores of the whole tile
             const long o0 = tile * TO;
@@ -990,11 +1053,14 @@ __global__ __launch_bounds__(kFirBlock) void fir_tile_f32(DecimLaunch a) {
 // Persistent variant for <= kFirStreamTaps taps (the headline decimator's
 // memory schedule): grid-stride tile order, the next tile's buffer loads
 // (non-temporal, range-checked zero fill past the end) issued into VGPRs
-// right after this tile lands in LDS, outputs staged back through LDS into
-// whole-line non-temporal stores.
+// right after this tile lands in LDS, outputs transposed across the wave's
+// lanes into whole-line non-temporal stores (OST below).
 constexpr int kFirStreamTaps = 128;
 
-template <int KV, bool FMA>
+// OST: 1 = outputs staged through LDS (two more barriers per tile); 2 = the
+// wave's outputs transposed across lanes (store_wave_lines) into whole-line
+// stores, no LDS round trip.
+template <int KV, bool FMA, int OST = 2>
 __global__ __launch_bounds__(kFirBlock, 4) void fir_stream_f32(DecimLaunch a) {
     typedef typename FirTraits<KV>::S S;
     constexpr int SPG = FirTraits<KV>::SPG;
@@ -1073,6 +1139,16 @@ __global__ __launch_bounds__(kFirBlock, 4) void fir_stream_f32(DecimLaunch a) {
         float2 o[R];
         fir_lane<KV, FMA>(fl, (P0 + R * t) / SPG, N, tp, a.shift, o);
         const long o0 = tile * TO;
+        if constexpr (OST == 2) {
+            if constexpr (WHOLE) {
+                store_wave_lines<R, true>(out + o0 + (t & ~63) * R, o, t & 63);
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    if (o0 + t * R + r < a.n_out) out[o0 + t * R + r] = o[r];
+            }
+            return;
+        }
         SRCDSP_LDS_BARRIER();  // every wave is done reading the staged input
         float2 *ob = (float2 *)fl;
 #pragma unroll
