@@ -269,7 +269,14 @@ __global__ __launch_bounds__(kUpBlockD) void up_tile_dot2(const uint32_t *in, lo
 #pragma unroll
         for (int r = 0; r < R; ++r) yr[o][r] = yi[o][r] = 0;
     ConstPtr<uint32_t> tp = const_view<uint32_t>(pairs);
-    uint32_t W0[4][4], W1[4][4];  // [plane][dword]
+    // Three window register sets rotate over the chunks and the taps of a
+    // chunk (4 pairs x LR phases, contiguous: dword (4q + pp) LR + o) arrive in
+    // one s_load; both for chunk q+1 are requested after chunk q's first pair,
+    // so the lgkmcnt wait at chunk q+1 lands three pairs of dot2 after them
+    // (waiting on a tap s_load drains every LDS read in flight too).
+    uint32_t W0[4][4], W1[4][4], W2[4][4];  // [plane][dword]
+    constexpr int TPC = 4 * LR;            // tap dwords per chunk
+    uint32_t Tc[TPC], Tn[TPC];
     auto load = [&](uint32_t (&w)[4][4], int gi) {
 #pragma unroll
         for (int pl4 = 0; pl4 < 4; ++pl4) {
@@ -277,16 +284,21 @@ __global__ __launch_bounds__(kUpBlockD) void up_tile_dot2(const uint32_t *in, lo
             w[pl4][0] = v.x; w[pl4][1] = v.y; w[pl4][2] = v.z; w[pl4][3] = v.w;
         }
     };
-    auto chunk = [&](int q, const uint32_t (&cur)[4][4], uint32_t (&nxt)[4][4]) {
+    auto load_taps = [&](uint32_t (&T)[TPC], int q) {
         asm volatile("" : "+s"(tp));
-        load(nxt, gb - q - 1);
+#pragma unroll
+        for (int i = 0; i < TPC; ++i) T[i] = tp[q * TPC + i];
+    };
+    const int NQ = (PP + 3) / 4;
+    auto chunk = [&](int q, const uint32_t (&cur)[4][4], const uint32_t (&nxt)[4][4], uint32_t (&nn)[4][4]) {
 #pragma unroll
         for (int pp = 0; pp < 4; ++pp) {
             const int p = 4 * q + pp;
-            if (p >= PP) break;
-            uint32_t P[LR];
-#pragma unroll
-            for (int o = 0; o < LR; ++o) P[o] = tp[o * PP + p];
+            if (p >= PP) break;  // the last chunk only
+            if (pp == 1 && q + 1 < NQ) {
+                load(nn, gb - q - 2);
+                load_taps(Tn, q + 1);
+            }
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int k = r >> 1, rel = k - pp;  // -3..3
@@ -295,22 +307,28 @@ __global__ __launch_bounds__(kUpBlockD) void up_tile_dot2(const uint32_t *in, lo
                 const uint32_t xi = rel >= 0 ? cur[pi][rel] : nxt[pi][rel + 4];
 #pragma unroll
                 for (int o = 0; o < LR; ++o) {
+                    const uint32_t P = Tc[pp * LR + o];
                     yr[o][r] = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t_u, xr),
-                                                      __builtin_bit_cast(short2_t_u, P[o]), yr[o][r], false);
+                                                      __builtin_bit_cast(short2_t_u, P), yr[o][r], false);
                     yi[o][r] = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t_u, xi),
-                                                      __builtin_bit_cast(short2_t_u, P[o]), yi[o][r], false);
+                                                      __builtin_bit_cast(short2_t_u, P), yi[o][r], false);
                 }
             }
         }
+#pragma unroll
+        for (int i = 0; i < TPC; ++i) Tc[i] = Tn[i];
     };
     load(W0, gb);
-    const int NQ = (PP + 3) / 4;
+    load(W1, gb - 1);
+    load_taps(Tc, 0);
     int q = 0;
-    for (; q + 2 <= NQ; q += 2) {
-        chunk(q, W0, W1);
-        chunk(q + 1, W1, W0);
+    for (; q + 3 <= NQ; q += 3) {
+        chunk(q, W0, W1, W2);
+        chunk(q + 1, W1, W2, W0);
+        chunk(q + 2, W2, W0, W1);
     }
-    if (q < NQ) chunk(q, W0, W1);
+    if (q < NQ) chunk(q, W0, W1, W2);
+    if (q + 1 < NQ) chunk(q + 1, W1, W2, W0);
     // outputs -> LDS (lane chunk of 8*LR words at a 9-granule stride for LR = 4,
     // conflict-free) -> whole-line 16-B stores of the tile's contiguous output
     constexpr int GPLo = R * LR / 4;    // output granules per lane
@@ -386,13 +404,16 @@ static int up_set(srcdsp_up_state &u, const void *coeffs, int n) {
     if (u.d_pair) (void)hipFree(u.d_pair);
     u.d_pair = nullptr;
     if (u.coef_i16) {  // tap pairs of each phase: (lo c_o[2p], hi c_o[2p-1]), c_o[-1] = c_o[H] = 0
-        const int Hh = n / (int)u.L, PP = Hh / 2 + 1;
-        std::vector<uint32_t> pr((size_t)u.L * PP);
+        // chunk-major for up_tile_dot2: the 4 pairs x L phases of chunk q are
+        // the contiguous dwords [4qL, 4(q+1)L), pair p of phase o at p L + o,
+        // zero-padded to whole chunks
+        const int Hh = n / (int)u.L, PP = Hh / 2 + 1, NQ = (PP + 3) / 4;
+        std::vector<uint32_t> pr((size_t)u.L * 4 * NQ, 0u);
         auto tap = [&](unsigned o, int i) {
             return (i >= 0 && i < Hh) ? (uint32_t)(uint16_t)(int16_t)c[o + (size_t)i * u.L] : 0u;
         };
         for (unsigned o = 0; o < u.L; ++o)
-            for (int q = 0; q < PP; ++q) pr[o * PP + q] = tap(o, 2 * q) | (tap(o, 2 * q - 1) << 16);
+            for (int q = 0; q < PP; ++q) pr[(size_t)q * u.L + o] = tap(o, 2 * q) | (tap(o, 2 * q - 1) << 16);
         SRCDSP_HIP_TRY(hipMalloc(&u.d_pair, 4 * pr.size()));
         SRCDSP_HIP_TRY(hipMemcpy(u.d_pair, pr.data(), 4 * pr.size(), hipMemcpyHostToDevice));
     }
