@@ -355,6 +355,56 @@ def cpu_baseline(args):
                       f"{secs:.2f} s; {src}; host CPU: {cpu}"}
 
 
+def cpu_baseline_allcores(args, threads=16):
+    """the reference on all the host cores this GPU's share of the box
+    gives (16 threads), one independent channel per thread (config 3's layout):
+    each thread owns a FilterDnsamplingFir object from oracle/_ref/strict and
+    steps its own channel; value = all threads' samples / the wall time from the
+    common start to the last thread's end.  ctypes drops the GIL for the calls."""
+    import threading
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    from srcdsp_amd.design import hamming_sinc
+    path = os.path.join(ROOT, "oracle", "_ref", "strict", "libref_decim_old.so")
+    if args.workload != "decim" or not os.path.exists(path):
+        return None
+    lib = C.CDLL(path)
+    lib.ref_decim_create.restype = C.c_void_p
+    lib.ref_decim_create.argtypes = [C.c_int, C.c_uint, C.c_void_p, C.c_int]
+    lib.ref_decim_step_timed.restype = C.c_double
+    lib.ref_decim_step_timed.argtypes = [C.c_void_p, C.c_void_p, C.c_long, C.c_void_p]
+    lib.ref_decim_destroy.argtypes = [C.c_void_p]
+    n = min(args.cpu_sample, args.samples) // 2
+    n -= n % 4
+    c = hamming_sinc(127)
+    o = pyoracle.Oracle(0)
+    xs = [o.gen_cf32(SEED, ch, 0, n) for ch in range(threads)]  # channel ch of the synthetic workload
+    ys = [np.zeros(n // 4, np.complex64) for _ in range(threads)]
+    hs = [lib.ref_decim_create(0, 4, c.ctypes.data, 127) for _ in range(threads)]
+    start = threading.Barrier(threads + 1)
+    ends = [0.0] * threads
+
+    def run(i):
+        start.wait()
+        lib.ref_decim_step_timed(hs[i], xs[i].ctypes.data, n, ys[i].ctypes.data)
+        ends[i] = time.perf_counter()
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(threads)]
+    for t in th:
+        t.start()
+    start.wait()
+    t0 = time.perf_counter()
+    for t in th:
+        t.join()
+    wall = max(ends) - t0
+    for h in hs:
+        lib.ref_decim_destroy(h)
+    return {"value": round(threads * n / wall / 1e6, 3), "unit": "Msamples/s", "cores": threads, "kind": "reference",
+            "sample": f"{threads} threads x {n} samples (channels 0..{threads - 1} of the synthetic workload, one "
+                      f"FilterDnsamplingFir per thread), {wall:.2f} s wall; oracle/_ref/strict/libref_decim_old.so; "
+                      f"host CPU: {_cpu_model()}"}
+
+
 def _cpu_model():
     try:
         with open("/proc/cpuinfo") as fh:
@@ -555,6 +605,8 @@ def main():
             line["detection"] = list(work.last)
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(args)
+            if args.workload == "decim":
+                line["cpu_baseline_allcores"] = cpu_baseline_allcores(args)
         if args.workload == "decim" and world == 1 and not args.no_pcie:
             line["pcie_inclusive"] = pcie_inclusive(S)
         print(json.dumps(line), flush=True)

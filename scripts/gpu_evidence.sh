@@ -26,7 +26,7 @@ for s in ${STEPS:-tests bench prof pmc}; do
       step bench_mixdecim_$TAG 300 python bench.py --workload mixdecim
       step bench_corr_$TAG 300 python bench.py --workload corr --samples 67108864
       step bench_fir_$TAG 300 python bench.py --workload fir
-      step bench_up_$TAG 300 python bench.py --workload up --no-cpu-baseline ;;
+      step bench_up_$TAG 300 python bench.py --workload up ;;
     prof)
       prof decim
       prof mixdecim
