@@ -161,6 +161,12 @@ extern "C" int tune_decim(int variant, int grid, const float *d_coef, const void
     case 72: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 2, true, 0, true, 2, true, true>, grid, 512, L, s);
     case 73: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 2, true, 2, true, true>, grid, 512, L, s);
     case 74: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 0, true, 2, true, true>, grid, 256, L, s);
+    // 12 waves per CU: 2 x 384 lanes or 1 x 768 lanes (up to 168 VGPRs)
+    case 92: L.ntiles = tiles(384 * 4); return launch(decim_stream2_cf32<127, 4, 384, true, 3, true, 0, true, 2, true, true>, grid, 384, L, s);
+    case 93: L.ntiles = tiles(768 * 4); return launch(decim_stream2_cf32<127, 4, 768, true, 3, true, 0, true, 2, true, true>, grid, 768, L, s);
+    case 94: L.ntiles = tiles(384 * 4); return launch(decim_stream2_cf32<127, 4, 384, true, 3, true, 1, true, 2, true, true>, grid, 384, L, s);
+    case 95: L.ntiles = tiles(768 * 4); return launch(decim_stream2_cf32<127, 4, 768, true, 3, true, 1, true, 2, true, true>, grid, 768, L, s);
+    case 96: L.ntiles = tiles(384 * 4); return launch(decim_stream2_cf32<127, 4, 384, true, 4, true, 0, true, 2, true, true>, grid, 384, L, s);
     case 75: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, 0, true, true>, grid, 512, L, s);
     case 24: L.ntiles = tiles(128 * 8); return launch(decim_stream2_cf32<127, 8, 128, true, 2, true>, grid, 128, L, s);
     default: return -1;

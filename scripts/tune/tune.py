@@ -109,6 +109,11 @@ def main():
                     (74, 2048, "OST2 256 g2048"), (75, 1024, "OST0 g1024"),
                     (71, 1024, "PROBE1 OST2 g1024"), (73, 1024, "PROBE2 OST2 g1024"), (110, 1024, "PROBE2 head g1024"),
                     (48, 1024, "head g1024 (again)"), (70, 1024, "OST2 g1024 (again)")]
+    if os.environ.get("TUNE_W12"):  # 12 waves per CU (2 x 384 or 1 x 768 lanes); PROBE1 = memory path only
+        variants = [(70, 1024, "head (OST2) g1024"), (92, 512, "384 mw3 g512"), (92, 1024, "384 mw3 g1024"),
+                    (96, 512, "384 mw4 g512"), (93, 256, "768 mw3 g256"), (93, 512, "768 mw3 g512"),
+                    (94, 512, "PROBE1 384 mw3 g512"), (95, 256, "PROBE1 768 mw3 g256"), (71, 1024, "PROBE1 head g1024"),
+                    (70, 1024, "head (again)")]
     if os.environ.get("TUNE_FIR"):
         fir_ab()
         return
