@@ -264,6 +264,53 @@ def test_headline_size_properties(S, O):
     torch.cuda.empty_cache()
 
 
+def test_config4_size_properties(S, O):
+    """Config 4 at full size (2^28 complex<int16_t>, device-resident, one fused
+    mixer -> decimator step): output windows (first tile, tile seams, random
+    interior, last tile) against the reference pair run on the same input
+    windows.  The oracle mixer is advanced to each window start by stepping
+    zeros (the phase does not depend on the data), so the NCO phase is checked
+    across the whole 2^28-sample call, and the oracle decimator starts each
+    window 128 samples early with an empty history."""
+    import torch
+    from srcdsp_amd.design import hamming_sinc, q14
+    cq = q14(hamming_sinc(127))
+    L = 1 << 28
+    x = torch.empty((L, 2), dtype=torch.int16, device="cuda")
+    S.fill_synthetic(x, "ci16", seed=0x5EED, channel=0, lo=-8192, hi=8191)
+    m = S.Mixer(4096)
+    m.reset(0.1)
+    d = S.FilterDnsamplingFir(cq, 4, "complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int32_t")
+    y = S.MixerDecimatorChain(m, d).step(x)
+    torch.cuda.synchronize()
+    om = O["strict"].mixer(4096)
+    om.reset(0.1)
+    n_out, TO = L // 4, 2048
+    rng = np.random.default_rng(4)
+    starts = sorted({0, 40, TO - 3, 2 * TO - 3, 7 * TO + 5, n_out - 1000, *map(int, rng.integers(64, n_out - 1000, 10))})
+    zeros = np.zeros((1 << 22, 2), np.int16)
+    pos = 0  # samples the oracle mixer has consumed
+    for s0 in starts:
+        lo = max(0, 4 * s0 - 128)
+        hi = 4 * (s0 + 64)
+        if lo < pos:  # overlapping windows: take the next one from where the mixer is
+            continue
+        while pos < lo:
+            k = min(lo - pos, len(zeros))
+            om.step(zeros[:k])
+            pos += k
+        xin = x[lo:hi].cpu().numpy()
+        assert np.array_equal(xin, O["strict"].gen_ci16(0x5EED, 0, lo, hi - lo, -8192, 8191))
+        mixed = om.step(xin)
+        pos = hi
+        od = O["strict"].decim(1, 4, cq)
+        r = od.step(mixed)[(4 * s0 - lo) // 4:]
+        got = y[s0:s0 + 64].cpu().numpy()
+        assert np.array_equal(got, r[:len(got)]), s0
+    del x, y
+    torch.cuda.empty_cache()
+
+
 # ----------------------------------------------------- other operators
 def test_mixer_large_vs_oracle(S, O):
     x = O["fma"].gen_ci16(11, 0, 0, (1 << 20) + 3, -32768, 32767)
