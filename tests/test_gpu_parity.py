@@ -417,6 +417,36 @@ def test_correlator_vs_oracle(S, O, N, S_):
     assert events >= 1
 
 
+def test_config5_size_properties(S, O):
+    """Config 5 at full size (2^26 samples, device-resident, one step): the
+    bench's buffer (noise +-125, the 1024-sample QPSK pattern x2 at 3/4).  The
+    GPU scan's first detection, bitSamples and registers equal the reference's
+    on a window around the hit, the reference primed with the samples before
+    the window (the registers after a detection-free stream depend only on the
+    last N*S+2 samples)."""
+    from srcdsp_amd import dist as D
+    from srcdsp_amd.design import qpsk_pattern
+    L = 1 << 26
+    p = qpsk_pattern(1024, 500, seed=2)
+    rng = np.random.default_rng(0)
+    x = rng.integers(-125, 126, size=(L, 2)).astype(np.int32)
+    off = (3 * L) // 4
+    x[off:off + 1024] += 2 * p
+    x = np.clip(x, -32768, 32767).astype(np.int16)
+    g = S.FixedPatternCorrelator(1024, 1)
+    g.setPattern(p)
+    fg, ig = g.step(dev(x))
+    r = O["fma"].corr(1024, 1)
+    r.set_pattern(p)
+    w0 = off - 4096
+    r.prime(x[w0 - D.corr_halo(1024, 1):w0])
+    fr, ir = r.step(x[w0:w0 + 8192])
+    assert fg and fr and ig == w0 + ir
+    assert np.array_equal(g.getRefBitSamples(), r.bit_samples())
+    st, sr = g.getStatus(), r.status()
+    assert all(st[k] == sr[k] for k in ("energy", "corr", "coeffs_energy", "coeff_scaling"))
+
+
 def test_time_split_segments_equal_single_call(S, O):
     """SURVEY 8e, one long buffer split in time (W = 3 segments run one after
     another here, as 3 ranks would): decimator seeded by stepping its halo,
