@@ -311,6 +311,38 @@ def test_config4_size_properties(S, O):
     torch.cuda.empty_cache()
 
 
+def test_fir_and_up_bench_size_properties(S, O):
+    """The fir and up bench workloads at their full sizes (2^28 float samples
+    through the 31-tap FilterFir<float,cf32,float,float>; 2^26 ci16 inputs
+    through the 128-tap x4 interpolator): output windows against the reference
+    run on the same input windows, started early enough to fill the history."""
+    import torch
+    from srcdsp_amd.design import hamming_sinc, q14
+    rng = np.random.default_rng(5)
+    L = 1 << 28
+    x = torch.randint(-2048, 2048, (L,), device="cuda").float()
+    c = hamming_sinc(31, 0.2)
+    y = S.FilterFir(c, "float", "complex<float>", "float", "float", fp="fma").step(x)
+    torch.cuda.synchronize()
+    for s0 in [0, 17, 8191, L - 64, *map(int, rng.integers(32, L - 64, 8))]:
+        lo = max(0, s0 - 32)
+        r = O["fma"].fir(1, c).step(x[lo:s0 + 64].cpu().numpy())[s0 - lo:]
+        assert np.array_equal(y[s0:s0 + 64].cpu().numpy(), r), s0
+    del x, y
+    n = 1 << 26
+    xu = torch.empty((n, 2), dtype=torch.int16, device="cuda")
+    S.fill_synthetic(xu, "ci16", seed=0x5EED, channel=0, lo=-8192, hi=8191)
+    cu = q14(hamming_sinc(128, 0.12) * 4)
+    yu = S.FilterUpsamplingFir(cu, 4).step(xu)
+    torch.cuda.synchronize()
+    for j0 in [0, 5, 2047, n - 64, *map(int, rng.integers(40, n - 64, 8))]:
+        lo = max(0, j0 - 40)
+        r = O["fma"].up(0, 4, cu).step(xu[lo:j0 + 64].cpu().numpy())[4 * (j0 - lo):]
+        assert np.array_equal(yu[4 * j0:4 * (j0 + 64)].cpu().numpy(), r), j0
+    del xu, yu
+    torch.cuda.empty_cache()
+
+
 # ----------------------------------------------------- other operators
 def test_mixer_large_vs_oracle(S, O):
     x = O["fma"].gen_ci16(11, 0, 0, (1 << 20) + 3, -32768, 32767)
