@@ -154,6 +154,21 @@ int launch_fir_tile(const DecimLaunch &L0, int channels, bool fma, hipStream_t s
     return SRCDSP_OK;
 }
 
+template <int M>
+int launch_decim_tile(const DecimLaunch &L0, int channels, bool fma, hipStream_t s) {
+    constexpr int TO = kDtBlock * (kDtRM / M);
+    DecimLaunch L = L0;
+    L.ntiles = (L.n_out + TO - 1) / TO;
+    const int nch = (L.ntaps + kDtRM - 1) / kDtRM;
+    const size_t smem = 16 * (size_t)kDtBS * (size_t)(nch + kDtBlock);
+    dim3 grid((unsigned)L.ntiles, channels);
+    if (fma)
+        hipLaunchKernelGGL((decim_tile_cf32<M, true>), grid, dim3(kDtBlock), smem, s, L);
+    else
+        hipLaunchKernelGGL((decim_tile_cf32<M, false>), grid, dim3(kDtBlock), smem, s, L);
+    return SRCDSP_OK;
+}
+
 template <int KV>
 int launch_generic(const DecimLaunch &L, int channels, unsigned M, bool fma, hipStream_t s) {
     long blocks = std::max<long>(1, std::min<long>((L.n_out + 255) / 256, 4096));
@@ -179,6 +194,10 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
                              : launch_fir_tile<KV_F32_REAL>(L, channels, fma, s);
     } else if (f.M == 4 && f.kv == KV_CF32 && al && (f.ntaps == 127 || f.ntaps == 128)) {
         rc = f.ntaps == 127 ? launch_cf32<127>(L, channels, fma, s) : launch_cf32<128>(L, channels, fma, s);
+    } else if (f.kv == KV_CF32 && (f.M == 2 || f.M == 4 || f.M == 8) && al && out_al && f.ntaps <= kDtMaxTaps &&
+               !mixed && L.n_out > 0) {
+        rc = f.M == 2 ? launch_decim_tile<2>(L, channels, fma, s)
+                      : (f.M == 4 ? launch_decim_tile<4>(L, channels, fma, s) : launch_decim_tile<8>(L, channels, fma, s));
     } else if (f.M == 4 && f.kv == KV_CI16_I32 && f.coef_fits_i16 && al && (f.ntaps == 127 || f.ntaps == 128)) {
         DecimLaunch L2 = L;
         L2.coef = f.d_cpair;
@@ -250,8 +269,11 @@ int FirCore::set_coeffs(const void *coeffs, int n, bool keep_history) {
         SRCDSP_HIP_TRY(hipMalloc(&d_cpair, 4 * (size_t)J));
         SRCDSP_HIP_TRY(hipMemcpy(d_cpair, pr.data(), 4 * (size_t)J, hipMemcpyHostToDevice));
     }
-    SRCDSP_HIP_TRY(hipMalloc(&d_coef, 4 * (size_t)n));
-    SRCDSP_HIP_TRY(hipMemcpy(d_coef, tmp.data(), 4 * (size_t)n, hipMemcpyHostToDevice));
+    // 16 zero taps of slack: the tap chunks of decim_tile_cf32 end on 16-tap
+    // boundaries (taps past N are never applied, but their s_load stays in bounds)
+    tmp.resize(4 * ((size_t)n + 16), '\0');
+    SRCDSP_HIP_TRY(hipMalloc(&d_coef, tmp.size()));
+    SRCDSP_HIP_TRY(hipMemcpy(d_coef, tmp.data(), tmp.size(), hipMemcpyHostToDevice));
 
     // history: resize keeping the first min(old,new) entries (vector::resize)
     const size_t es = kv_in_bytes(kv);

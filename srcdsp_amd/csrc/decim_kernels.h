@@ -672,6 +672,105 @@ __device__ __forceinline__ void mix_dot2(uint32_t w, uint32_t C, int32_t &re, in
     im = clamp_s14(sdot2(ws, C, 0));
 }
 
+// Tiled complex<float> decimator for any tap count (<= kDtMaxTaps) at M in
+// {2, 4, 8} (dnsampling_filters.h:129-172 off the headline's 127/128-tap
+// M=4 shape).  A lane owns R = 16/M consecutive outputs, i.e. one 16-sample
+// block b = lane of the tile's input image; output r, tap k reads sample
+// r*M - k of the lane's block frame.  Taps run in chunks of 16 (one SGPR
+// s_load each); chunk c touches blocks b-c ("cur") and b-c-1 ("nxt"), so three
+// 16-sample register windows rotate over the chunks (the next chunk's window
+// is read from LDS while this one's FMAs run).  Each output is one sequential
+// fma (or mul+add) chain in ascending k; taps past N are skipped, never
+// multiplied by zero (0 * inf would differ).  LDS blocks are 8 granules + one
+// pad granule, so the lanes' ds_read_b128 are conflict-free.  One tile per
+// workgroup; the image holds ceil(N/16) halo blocks before the tile.
+constexpr int kDtBlock = 256, kDtRM = 16, kDtMaxTaps = 1024;
+constexpr int kDtBS = kDtRM / 2 + 1;  // LDS granules per block (pad included)
+
+template <int M, bool FMA>
+__global__ __launch_bounds__(kDtBlock) void decim_tile_cf32(DecimLaunch a) {
+    static_assert(kDtRM % M == 0, "M divides the block");
+    constexpr int R = kDtRM / M, RM = kDtRM, TO = kDtBlock * R;
+    extern __shared__ float4 dimg[];
+    const int ch = blockIdx.y;
+    const float2 *in = (const float2 *)a.in + ch * a.in_stride;
+    const float2 *hist = (const float2 *)a.hist_in[ch];
+    float2 *out = (float2 *)a.out + ch * a.out_stride;
+    const long n_in = a.n_in;
+    const int N = a.ntaps, H = N - 1;
+    const int NCH = (N + RM - 1) / RM;  // tap chunks = halo blocks
+    const int t = threadIdx.x;
+    const long tile = blockIdx.x;
+    if (tile == 0) write_history(in, n_in, hist, (float2 *)a.hist_out[ch], H);
+    // image block i holds samples s0 + 16 i .. s0 + 16 i + 15
+    const long s0 = tile * (long)TO * M - (long)NCH * RM;
+    const int NG = (NCH + kDtBlock) * (RM / 2);  // 2-sample granules
+    for (int g = t; g < NG; g += kDtBlock) {
+        const long s = s0 + 2L * g;
+        float4 v;
+        if (s >= 0 && s + 1 < n_in) {
+            v = *(const float4 *)(in + s);
+        } else {
+            const float2 lo = fetch(in, hist, s, n_in, H), hi = fetch(in, hist, s + 1, n_in, H);
+            v = make_float4(lo.x, lo.y, hi.x, hi.y);
+        }
+        dimg[(g / (RM / 2)) * kDtBS + g % (RM / 2)] = v;
+    }
+    __syncthreads();
+    float2 W0[RM], W1[RM], W2[RM];
+    auto load = [&](float2 (&w)[RM], int blk) {
+#pragma unroll
+        for (int i = 0; i < RM / 2; ++i) {
+            const float4 v = dimg[blk * kDtBS + i];
+            w[2 * i] = make_float2(v.x, v.y);
+            w[2 * i + 1] = make_float2(v.z, v.w);
+        }
+    };
+    float yr[R], yi[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) yr[r] = yi[r] = 0.f;
+    const int me = NCH + t;  // the lane's own block
+    ConstPtr<float> tp = const_view<float>(a.coef);
+    auto chunk = [&](int c, const float2 (&cur)[RM], const float2 (&nxt)[RM], float2 (&nn)[RM]) {
+        asm volatile("" : "+s"(tp));
+        if (c + 1 < NCH) load(nn, me - c - 2);
+#pragma unroll
+        for (int i = 0; i < RM; ++i) {
+            const int k = c * RM + i;
+            if (k >= N) break;
+            const float cf = tp[k];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int l = r * M - i;
+                const float2 x = l >= 0 ? cur[l] : nxt[l + RM];
+                yr[r] = mac<FMA>(cf, x.x, yr[r]);
+                yi[r] = mac<FMA>(cf, x.y, yi[r]);
+            }
+        }
+    };
+    load(W0, me);
+    load(W1, me - 1);
+    int c = 0;
+    for (; c + 3 <= NCH; c += 3) {
+        chunk(c, W0, W1, W2);
+        chunk(c + 1, W1, W2, W0);
+        chunk(c + 2, W2, W0, W1);
+    }
+    if (c < NCH) chunk(c, W0, W1, W2);
+    if (c + 1 < NCH) chunk(c + 1, W1, W2, W0);
+    const long o0 = tile * TO + (long)t * R;
+    if (o0 + R <= a.n_out) {
+#pragma unroll
+        for (int r = 0; r < R; r += 2)
+            *(float4 *)(out + o0 + r) = make_float4(q16f(yr[r], a.shift), q16f(yi[r], a.shift),
+                                                    q16f(yr[r + 1], a.shift), q16f(yi[r + 1], a.shift));
+    } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (o0 + r < a.n_out) out[o0 + r] = make_float2(q16f(yr[r], a.shift), q16f(yi[r], a.shift));
+    }
+}
+
 // TAB2 (mixer): the (lr, li) table stored twice (2N words), so the address of
 // sample j of staged granule i is one add of a wave-uniform tile/granule
 // phase (SGPR) and a per-lane constant (4t + j)*freq mod N -- no per-sample

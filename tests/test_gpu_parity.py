@@ -79,6 +79,23 @@ def test_decim_cf32_tile_kernel_vs_oracle(S, O, fp, ntaps):
         assert np.array_equal(y.view(np.uint32), ref.step(xs).view(np.uint32)), (off, n)
 
 
+@pytest.mark.parametrize("fp", ["fma", "strict"])
+@pytest.mark.parametrize("M,ntaps", [(2, 1), (2, 16), (2, 17), (2, 63), (2, 128), (4, 2), (4, 15), (4, 48),
+                                     (4, 63), (4, 255), (4, 1024), (8, 8), (8, 49), (8, 255), (8, 1000)])
+def test_decim_cf32_any_taps_tile_vs_oracle(S, O, fp, M, ntaps):
+    """decim_tile_cf32 (M in 2/4/8, runtime tap count <= 1024): tail tiles,
+    calls shorter than the filter, chained uneven calls, both float contracts."""
+    rng = np.random.default_rng(M * 10000 + ntaps)
+    c = (rng.standard_normal(ntaps) / max(2, ntaps) ** 0.5).astype(np.float32)
+    x = O[fp].gen_cf32(33 + ntaps, M, 0, 200000)
+    g = S.FilterDnsamplingFir(c, M, fp=fp)
+    r = O[fp].decim(0, M, c)
+    for off, n in _chunks(len(x), [65536, M, 8 * M, 70000, 4 * M * 1000 + 8]):
+        n -= n % M
+        xs = x[off:off + n]
+        assert np.array_equal(g.step(dev(xs)).cpu().numpy(), r.step(xs)), (off, n)
+
+
 def test_decim_fma_vs_strict_tolerance(S, O):
     """Stated float tolerance: the FMA contract differs from the
     -O2 x86-64 reference by at most 1 output LSB on at most 1e-4 of outputs."""
