@@ -154,19 +154,25 @@ int launch_fir_tile(const DecimLaunch &L0, int channels, bool fma, hipStream_t s
     return SRCDSP_OK;
 }
 
-template <int M>
-int launch_decim_tile(const DecimLaunch &L0, int channels, bool fma, hipStream_t s) {
+template <int KV, int M, int P>
+int launch_decim_tile(const DecimLaunch &L0, int channels, hipStream_t s) {
     constexpr int TO = kDtBlock * (kDtRM / M);
     DecimLaunch L = L0;
     L.ntiles = (L.n_out + TO - 1) / TO;
     const int nch = (L.ntaps + kDtRM - 1) / kDtRM;
     const size_t smem = 16 * (size_t)kDtBS * (size_t)(nch + kDtBlock);
     dim3 grid((unsigned)L.ntiles, channels);
-    if (fma)
-        hipLaunchKernelGGL((decim_tile_cf32<M, true>), grid, dim3(kDtBlock), smem, s, L);
-    else
-        hipLaunchKernelGGL((decim_tile_cf32<M, false>), grid, dim3(kDtBlock), smem, s, L);
+    hipLaunchKernelGGL((decim_tile<KV, M, P>), grid, dim3(kDtBlock), smem, s, L);
     return SRCDSP_OK;
+}
+
+template <int KV, int P>
+int launch_decim_tile_m(const DecimLaunch &L, int channels, unsigned M, hipStream_t s) {
+    switch (M) {
+    case 2: return launch_decim_tile<KV, 2, P>(L, channels, s);
+    case 4: return launch_decim_tile<KV, 4, P>(L, channels, s);
+    default: return launch_decim_tile<KV, 8, P>(L, channels, s);
+    }
 }
 
 template <int KV>
@@ -181,6 +187,7 @@ int launch_generic(const DecimLaunch &L, int channels, unsigned M, bool fma, hip
 }
 
 bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
+bool aligned8(const void *p) { return ((uintptr_t)p & 7u) == 0; }
 }  // namespace
 
 // Choose the kernel for one FirCore configuration and launch it.
@@ -194,16 +201,25 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
                              : launch_fir_tile<KV_F32_REAL>(L, channels, fma, s);
     } else if (f.M == 4 && f.kv == KV_CF32 && al && (f.ntaps == 127 || f.ntaps == 128)) {
         rc = f.ntaps == 127 ? launch_cf32<127>(L, channels, fma, s) : launch_cf32<128>(L, channels, fma, s);
-    } else if (f.kv == KV_CF32 && (f.M == 2 || f.M == 4 || f.M == 8) && al && out_al && f.ntaps <= kDtMaxTaps &&
-               !mixed && L.n_out > 0) {
-        rc = f.M == 2 ? launch_decim_tile<2>(L, channels, fma, s)
-                      : (f.M == 4 ? launch_decim_tile<4>(L, channels, fma, s) : launch_decim_tile<8>(L, channels, fma, s));
     } else if (f.M == 4 && f.kv == KV_CI16_I32 && f.coef_fits_i16 && al && (f.ntaps == 127 || f.ntaps == 128)) {
         DecimLaunch L2 = L;
         L2.coef = f.d_cpair;
         rc = f.ntaps == 127 ? launch_ci16_dot2<127>(L2, channels, mixed, s) : launch_ci16_dot2<128>(L2, channels, mixed, s);
     } else if (f.M == 4 && f.kv == KV_CI16_I32 && f.coef_fits_i24 && al && (f.ntaps == 127 || f.ntaps == 128)) {
         rc = f.ntaps == 127 ? launch_ci16<127>(L, channels, mixed, s) : launch_ci16<128>(L, channels, mixed, s);
+    } else if ((f.kv == KV_CF32 || f.kv == KV_CI16_I32 || f.kv == KV_CI16_I16) && (f.M == 2 || f.M == 4 || f.M == 8) &&
+               (f.kv == KV_CF32 ? al : aligned8(L.in) && (L.in_stride * 4) % 8 == 0) &&
+               (f.kv == KV_CF32 ? out_al : aligned8(L.out) && (L.out_stride * 4) % 8 == 0) &&
+               f.ntaps <= kDtMaxTaps && !mixed && L.n_out > 0) {
+        // any tap count <= 1024 at M = 2/4/8
+        if (f.kv == KV_CF32)
+            rc = fma ? launch_decim_tile_m<KV_CF32, 1>(L, channels, f.M, s) : launch_decim_tile_m<KV_CF32, 0>(L, channels, f.M, s);
+        else if (f.kv == KV_CI16_I16)
+            rc = launch_decim_tile_m<KV_CI16_I16, 2>(L, channels, f.M, s);
+        else if (f.coef_fits_i24)
+            rc = launch_decim_tile_m<KV_CI16_I32, 0>(L, channels, f.M, s);
+        else
+            rc = launch_decim_tile_m<KV_CI16_I32, 1>(L, channels, f.M, s);
     } else {
         if (mixed) {
             set_error("mixer->decimator fusion needs variant 1, M=4, 127/128 taps |c|<2^23, 16-B aligned input");

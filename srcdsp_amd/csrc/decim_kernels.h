@@ -672,79 +672,118 @@ __device__ __forceinline__ void mix_dot2(uint32_t w, uint32_t C, int32_t &re, in
     im = clamp_s14(sdot2(ws, C, 0));
 }
 
-// Tiled complex<float> decimator for any tap count (<= kDtMaxTaps) at M in
-// {2, 4, 8} (dnsampling_filters.h:129-172 off the headline's 127/128-tap
-// M=4 shape).  A lane owns R = 16/M consecutive outputs, i.e. one 16-sample
-// block b = lane of the tile's input image; output r, tap k reads sample
-// r*M - k of the lane's block frame.  Taps run in chunks of 16 (one SGPR
-// s_load each); chunk c touches blocks b-c ("cur") and b-c-1 ("nxt"), so three
-// 16-sample register windows rotate over the chunks (the next chunk's window
-// is read from LDS while this one's FMAs run).  Each output is one sequential
-// fma (or mul+add) chain in ascending k; taps past N are skipped, never
-// multiplied by zero (0 * inf would differ).  LDS blocks are 8 granules + one
-// pad granule, so the lanes' ds_read_b128 are conflict-free.  One tile per
+// Tiled decimator for any tap count (<= kDtMaxTaps) at M in {2, 4, 8}
+// (dnsampling_filters.h:129-172 off the headline's 127/128-tap M=4 shape),
+// complex<float> (KV_CF32; P = 1: fma chain, 0: mul+add) or complex<int16_t>
+// with int32 (KV_CI16_I32; P = 0: |c| < 2^23 as v_mad_i32_i24, 1: full 32-bit
+// products) or int16 taps (KV_CI16_I16, P = 2: products wrapped to int16).
+// A lane owns R = 16/M consecutive outputs, i.e. one 16-sample block b = lane
+// of the tile's input image; output r, tap k reads sample r*M - k of the
+// lane's block frame.  Taps run in chunks of 16 (one SGPR s_load each); chunk
+// c touches blocks b-c ("cur") and b-c-1 ("nxt"), so three 16-sample register
+// windows rotate over the chunks (the next chunk's window is read from LDS
+// while this one's MACs run).  Each output is one sequential chain in
+// ascending k; taps past N are skipped, never multiplied by zero (0 * inf
+// would differ).  ci16 samples are split into int32 (re, im) while staging,
+// so the image has the cf32 layout: LDS blocks are 8 granules + one pad
+// granule and the lanes' ds_read_b128 are conflict-free.  One tile per
 // workgroup; the image holds ceil(N/16) halo blocks before the tile.
 constexpr int kDtBlock = 256, kDtRM = 16, kDtMaxTaps = 1024;
 constexpr int kDtBS = kDtRM / 2 + 1;  // LDS granules per block (pad included)
 
-template <int M, bool FMA>
-__global__ __launch_bounds__(kDtBlock) void decim_tile_cf32(DecimLaunch a) {
+template <int KV, int M, int P>
+__global__ __launch_bounds__(kDtBlock) void decim_tile(DecimLaunch a) {
     static_assert(kDtRM % M == 0, "M divides the block");
+    static_assert(KV == KV_CF32 || KV == KV_CI16_I32 || KV == KV_CI16_I16, "sample kinds");
+    constexpr bool CF = KV == KV_CF32;
+    typedef typename std::conditional<CF, float2, int2>::type X2;
+    typedef typename std::conditional<CF, float2, uint32_t>::type SIn;
     constexpr int R = kDtRM / M, RM = kDtRM, TO = kDtBlock * R;
     extern __shared__ float4 dimg[];
     const int ch = blockIdx.y;
-    const float2 *in = (const float2 *)a.in + ch * a.in_stride;
-    const float2 *hist = (const float2 *)a.hist_in[ch];
-    float2 *out = (float2 *)a.out + ch * a.out_stride;
+    const SIn *in = (const SIn *)a.in + ch * a.in_stride;
+    const SIn *hist = (const SIn *)a.hist_in[ch];
     const long n_in = a.n_in;
     const int N = a.ntaps, H = N - 1;
     const int NCH = (N + RM - 1) / RM;  // tap chunks = halo blocks
     const int t = threadIdx.x;
     const long tile = blockIdx.x;
-    if (tile == 0) write_history(in, n_in, hist, (float2 *)a.hist_out[ch], H);
-    // image block i holds samples s0 + 16 i .. s0 + 16 i + 15
+    if (tile == 0) write_history(in, n_in, hist, (SIn *)a.hist_out[ch], H);
+    // image block i holds samples s0 + 16 i .. s0 + 16 i + 15, as (re, im) pairs
     const long s0 = tile * (long)TO * M - (long)NCH * RM;
     const int NG = (NCH + kDtBlock) * (RM / 2);  // 2-sample granules
     for (int g = t; g < NG; g += kDtBlock) {
         const long s = s0 + 2L * g;
         float4 v;
-        if (s >= 0 && s + 1 < n_in) {
-            v = *(const float4 *)(in + s);
+        if constexpr (CF) {
+            if (s >= 0 && s + 1 < n_in) {
+                v = *(const float4 *)(in + s);
+            } else {
+                const float2 lo = fetch(in, hist, s, n_in, H), hi = fetch(in, hist, s + 1, n_in, H);
+                v = make_float4(lo.x, lo.y, hi.x, hi.y);
+            }
         } else {
-            const float2 lo = fetch(in, hist, s, n_in, H), hi = fetch(in, hist, s + 1, n_in, H);
-            v = make_float4(lo.x, lo.y, hi.x, hi.y);
+            uint32_t w0, w1;
+            if (s >= 0 && s + 1 < n_in) {
+                const uint2 w = *(const uint2 *)(in + s);
+                w0 = w.x;
+                w1 = w.y;
+            } else {
+                w0 = fetch(in, hist, s, n_in, H);
+                w1 = fetch(in, hist, s + 1, n_in, H);
+            }
+            v = make_float4(__int_as_float(sext16(w0)), __int_as_float(sext16_hi(w0)), __int_as_float(sext16(w1)),
+                            __int_as_float(sext16_hi(w1)));
         }
         dimg[(g / (RM / 2)) * kDtBS + g % (RM / 2)] = v;
     }
     __syncthreads();
-    float2 W0[RM], W1[RM], W2[RM];
-    auto load = [&](float2 (&w)[RM], int blk) {
+    X2 W0[RM], W1[RM], W2[RM];
+    auto load = [&](X2 (&w)[RM], int blk) {
 #pragma unroll
         for (int i = 0; i < RM / 2; ++i) {
             const float4 v = dimg[blk * kDtBS + i];
-            w[2 * i] = make_float2(v.x, v.y);
-            w[2 * i + 1] = make_float2(v.z, v.w);
+            if constexpr (CF) {
+                w[2 * i] = make_float2(v.x, v.y);
+                w[2 * i + 1] = make_float2(v.z, v.w);
+            } else {
+                w[2 * i] = make_int2(__float_as_int(v.x), __float_as_int(v.y));
+                w[2 * i + 1] = make_int2(__float_as_int(v.z), __float_as_int(v.w));
+            }
         }
     };
-    float yr[R], yi[R];
+    typedef typename std::conditional<CF, float, uint32_t>::type Acc;
+    Acc yr[R], yi[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) yr[r] = yi[r] = 0.f;
+    for (int r = 0; r < R; ++r) yr[r] = yi[r] = Acc{};
     const int me = NCH + t;  // the lane's own block
-    ConstPtr<float> tp = const_view<float>(a.coef);
-    auto chunk = [&](int c, const float2 (&cur)[RM], const float2 (&nxt)[RM], float2 (&nn)[RM]) {
+    typedef typename std::conditional<CF, float, int32_t>::type Tap;
+    ConstPtr<Tap> tp = const_view<Tap>(a.coef);
+    auto chunk = [&](int c, const X2 (&cur)[RM], const X2 (&nxt)[RM], X2 (&nn)[RM]) {
         asm volatile("" : "+s"(tp));
         if (c + 1 < NCH) load(nn, me - c - 2);
 #pragma unroll
         for (int i = 0; i < RM; ++i) {
             const int k = c * RM + i;
             if (k >= N) break;
-            const float cf = tp[k];
+            const Tap cf = tp[k];
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int l = r * M - i;
-                const float2 x = l >= 0 ? cur[l] : nxt[l + RM];
-                yr[r] = mac<FMA>(cf, x.x, yr[r]);
-                yi[r] = mac<FMA>(cf, x.y, yi[r]);
+                const X2 x = l >= 0 ? cur[l] : nxt[l + RM];
+                if constexpr (CF) {
+                    yr[r] = mac<P == 1>(cf, x.x, yr[r]);
+                    yi[r] = mac<P == 1>(cf, x.y, yi[r]);
+                } else if constexpr (P == 0) {  // |c| < 2^23: the low 32 bits of the exact product
+                    yr[r] += (uint32_t)__mul24(cf, x.x);
+                    yi[r] += (uint32_t)__mul24(cf, x.y);
+                } else if constexpr (P == 1) {
+                    yr[r] += (uint32_t)cf * (uint32_t)x.x;
+                    yi[r] += (uint32_t)cf * (uint32_t)x.y;
+                } else {  // std::operator*(short, complex<short>): int16 wrap
+                    yr[r] += (uint32_t)sext16((uint32_t)__mul24(cf, x.x));
+                    yi[r] += (uint32_t)sext16((uint32_t)__mul24(cf, x.y));
+                }
             }
         }
     };
@@ -759,15 +798,31 @@ __global__ __launch_bounds__(kDtBlock) void decim_tile_cf32(DecimLaunch a) {
     if (c < NCH) chunk(c, W0, W1, W2);
     if (c + 1 < NCH) chunk(c + 1, W1, W2, W0);
     const long o0 = tile * TO + (long)t * R;
-    if (o0 + R <= a.n_out) {
+    if constexpr (CF) {
+        float2 *out = (float2 *)a.out + ch * a.out_stride;
+        if (o0 + R <= a.n_out) {
 #pragma unroll
-        for (int r = 0; r < R; r += 2)
-            *(float4 *)(out + o0 + r) = make_float4(q16f(yr[r], a.shift), q16f(yi[r], a.shift),
-                                                    q16f(yr[r + 1], a.shift), q16f(yi[r + 1], a.shift));
+            for (int r = 0; r < R; r += 2)
+                *(float4 *)(out + o0 + r) = make_float4(q16f(yr[r], a.shift), q16f(yi[r], a.shift),
+                                                        q16f(yr[r + 1], a.shift), q16f(yi[r + 1], a.shift));
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (o0 + r < a.n_out) out[o0 + r] = make_float2(q16f(yr[r], a.shift), q16f(yi[r], a.shift));
+        }
     } else {
+        uint32_t *out = (uint32_t *)a.out + ch * a.out_stride;
+        uint32_t w[R];
 #pragma unroll
-        for (int r = 0; r < R; ++r)
-            if (o0 + r < a.n_out) out[o0 + r] = make_float2(q16f(yr[r], a.shift), q16f(yi[r], a.shift));
+        for (int r = 0; r < R; ++r) w[r] = pack16(limit16((int32_t)yr[r], a.shift), limit16((int32_t)yi[r], a.shift));
+        if (o0 + R <= a.n_out) {
+#pragma unroll
+            for (int r = 0; r < R; r += 2) *(uint2 *)(out + o0 + r) = make_uint2(w[r], w[r + 1]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (o0 + r < a.n_out) out[o0 + r] = w[r];
+        }
     }
 }
 

@@ -96,6 +96,32 @@ def test_decim_cf32_any_taps_tile_vs_oracle(S, O, fp, M, ntaps):
         assert np.array_equal(g.step(dev(xs)).cpu().numpy(), r.step(xs)), (off, n)
 
 
+@pytest.mark.parametrize("kind", ["i16", "i24", "i32", "t16"])
+@pytest.mark.parametrize("M,ntaps", [(2, 1), (2, 33), (2, 127), (4, 17), (4, 63), (4, 200), (8, 16), (8, 255),
+                                     (8, 1024)])
+def test_decim_ci16_any_taps_tile_vs_oracle(S, O, kind, M, ntaps):
+    """decim_tile for complex<int16_t> (M in 2/4/8, runtime tap count <= 1024):
+    int32 taps in int16 / i24 / wider range (v_mad_i32_i24 or full 32-bit
+    products) and int16 taps (products wrapped to int16, "t16"); full-scale
+    inputs so the accumulators wrap and the outputs saturate."""
+    rng = np.random.default_rng(M * 100 + ntaps + len(kind))
+    lim = {"i16": 32767, "i24": (1 << 23) - 1, "i32": 1 << 24, "t16": 32767}[kind]
+    c = rng.integers(-lim, lim + 1, size=ntaps).astype(np.int32)
+    c[0] = lim
+    x = O["strict"].gen_ci16(7 + ntaps, M, 0, 150000, -32768, 32767)
+    if kind == "t16":
+        c = c.astype(np.int16)
+        g = S.FilterDnsamplingFir(c, M, "complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int16_t")
+        r = O["strict"].decim(2, M, c)
+    else:
+        g = S.FilterDnsamplingFir(c, M, "complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int32_t")
+        r = O["strict"].decim(1, M, c)
+    for off, n in _chunks(len(x), [65536, M, 8 * M, 60000, 2 * M * 1000 + 4]):
+        n -= n % M
+        xs = x[off:off + n]
+        assert np.array_equal(g.step(dev(xs)).cpu().numpy(), r.step(xs)), (off, n)
+
+
 def test_decim_fma_vs_strict_tolerance(S, O):
     """Stated float tolerance: the FMA contract differs from the
     -O2 x86-64 reference by at most 1 output LSB on at most 1e-4 of outputs."""
