@@ -169,6 +169,7 @@ int launch_decim_tile(const DecimLaunch &L0, int channels, hipStream_t s) {
 template <int KV, int P>
 int launch_decim_tile_m(const DecimLaunch &L, int channels, unsigned M, hipStream_t s) {
     switch (M) {
+    case 1: return launch_decim_tile<KV, 1, P>(L, channels, s);
     case 2: return launch_decim_tile<KV, 2, P>(L, channels, s);
     case 4: return launch_decim_tile<KV, 4, P>(L, channels, s);
     default: return launch_decim_tile<KV, 8, P>(L, channels, s);
@@ -207,11 +208,12 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
         rc = f.ntaps == 127 ? launch_ci16_dot2<127>(L2, channels, mixed, s) : launch_ci16_dot2<128>(L2, channels, mixed, s);
     } else if (f.M == 4 && f.kv == KV_CI16_I32 && f.coef_fits_i24 && al && (f.ntaps == 127 || f.ntaps == 128)) {
         rc = f.ntaps == 127 ? launch_ci16<127>(L, channels, mixed, s) : launch_ci16<128>(L, channels, mixed, s);
-    } else if ((f.kv == KV_CF32 || f.kv == KV_CI16_I32 || f.kv == KV_CI16_I16) && (f.M == 2 || f.M == 4 || f.M == 8) &&
+    } else if ((f.kv == KV_CF32 || f.kv == KV_CI16_I32 || f.kv == KV_CI16_I16) &&
+               (f.M == 1 || f.M == 2 || f.M == 4 || f.M == 8) &&
                (f.kv == KV_CF32 ? al : aligned8(L.in) && (L.in_stride * 4) % 8 == 0) &&
                (f.kv == KV_CF32 ? out_al : aligned8(L.out) && (L.out_stride * 4) % 8 == 0) &&
                f.ntaps <= kDtMaxTaps && !mixed && L.n_out > 0) {
-        // any tap count <= 1024 at M = 2/4/8
+        // any tap count <= 1024 at M = 1/2/4/8 (M = 1: FilterFir on complex<int16_t>)
         if (f.kv == KV_CF32)
             rc = fma ? launch_decim_tile_m<KV_CF32, 1>(L, channels, f.M, s) : launch_decim_tile_m<KV_CF32, 0>(L, channels, f.M, s);
         else if (f.kv == KV_CI16_I16)

@@ -122,6 +122,24 @@ def test_decim_ci16_any_taps_tile_vs_oracle(S, O, kind, M, ntaps):
         assert np.array_equal(g.step(dev(xs)).cpu().numpy(), r.step(xs)), (off, n)
 
 
+@pytest.mark.parametrize("kind", ["i16", "i24", "i32"])
+@pytest.mark.parametrize("ntaps", [1, 16, 17, 31, 100, 1024])
+def test_fir_ci16_tile_vs_oracle(S, O, kind, ntaps):
+    """FilterFir<ci16,ci16,ci32,int32_t> (filters.h:131-169) on decim_tile with
+    M = 1: int32 taps in the three product ranges, full-scale inputs, chained
+    uneven calls."""
+    rng = np.random.default_rng(ntaps * 3 + len(kind))
+    lim = {"i16": 32767, "i24": (1 << 23) - 1, "i32": 1 << 24}[kind]
+    c = rng.integers(-lim, lim + 1, size=ntaps).astype(np.int32)
+    c[0] = lim
+    x = O["strict"].gen_ci16(5 + ntaps, 3, 0, 90000, -32768, 32767)
+    g = S.FilterFir(c, "complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int32_t")
+    r = O["strict"].fir(2, c)
+    for off, n in _chunks(len(x), [40000, 1, 7, 4096 + 3, 30000]):
+        xs = x[off:off + n]
+        assert np.array_equal(g.step(dev(xs)).cpu().numpy(), r.step(xs)), (off, n)
+
+
 def test_decim_fma_vs_strict_tolerance(S, O):
     """Stated float tolerance: the FMA contract differs from the
     -O2 x86-64 reference by at most 1 output LSB on at most 1e-4 of outputs."""
