@@ -712,7 +712,31 @@ __global__ __launch_bounds__(kDtBlock) void decim_tile(DecimLaunch a) {
     // image block i holds samples s0 + 16 i .. s0 + 16 i + 15, as (re, im) pairs
     const long s0 = tile * (long)TO * M - (long)NCH * RM;
     const int NG = (NCH + kDtBlock) * (RM / 2);  // 2-sample granules
-    for (int g = t; g < NG; g += kDtBlock) {
+    auto put = [&](int g, float4 v) { dimg[(g / (RM / 2)) * kDtBS + g % (RM / 2)] = v; };
+    auto split = [&](uint32_t w0, uint32_t w1) {
+        return make_float4(__int_as_float(sext16(w0)), __int_as_float(sext16_hi(w0)), __int_as_float(sext16(w1)),
+                           __int_as_float(sext16_hi(w1)));
+    };
+    // the tile's own span (every tile but the launch's last lies inside the
+    // input): all RM/2 granule loads of a lane issued before any lands in LDS
+    const int G0 = NCH * (RM / 2);
+    const bool body_in = (tile + 1) * (long)TO * M <= n_in;
+    if (body_in) {
+        float4 v[RM / 2];
+#pragma unroll
+        for (int i = 0; i < RM / 2; ++i) {
+            const long s = s0 + 2L * (G0 + t + i * kDtBlock);
+            if constexpr (CF) {
+                v[i] = *(const float4 *)(in + s);
+            } else {
+                const uint2 w = *(const uint2 *)(in + s);
+                v[i] = split(w.x, w.y);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < RM / 2; ++i) put(G0 + t + i * kDtBlock, v[i]);
+    }
+    for (int g = t; g < (body_in ? G0 : NG); g += kDtBlock) {
         const long s = s0 + 2L * g;
         float4 v;
         if constexpr (CF) {
@@ -732,10 +756,9 @@ __global__ __launch_bounds__(kDtBlock) void decim_tile(DecimLaunch a) {
                 w0 = fetch(in, hist, s, n_in, H);
                 w1 = fetch(in, hist, s + 1, n_in, H);
             }
-            v = make_float4(__int_as_float(sext16(w0)), __int_as_float(sext16_hi(w0)), __int_as_float(sext16(w1)),
-                            __int_as_float(sext16_hi(w1)));
+            v = split(w0, w1);
         }
-        dimg[(g / (RM / 2)) * kDtBS + g % (RM / 2)] = v;
+        put(g, v);
     }
     __syncthreads();
     X2 W0[RM], W1[RM], W2[RM];
