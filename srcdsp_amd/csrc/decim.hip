@@ -156,11 +156,11 @@ int launch_fir_tile(const DecimLaunch &L0, int channels, bool fma, hipStream_t s
 
 template <int KV, int M, int P>
 int launch_decim_tile(const DecimLaunch &L0, int channels, hipStream_t s) {
-    constexpr int TO = kDtBlock * (kDtRM / M);
+    constexpr int RM = dt_rm(M), TO = kDtBlock * (RM / M);
     DecimLaunch L = L0;
     L.ntiles = (L.n_out + TO - 1) / TO;
-    const int nch = (L.ntaps + kDtRM - 1) / kDtRM;
-    const size_t smem = 16 * (size_t)kDtBS * (size_t)(nch + kDtBlock);
+    const int nch = (L.ntaps + RM - 1) / RM;
+    const size_t smem = 16 * (size_t)dt_bs(M) * (size_t)(nch + kDtBlock);
     dim3 grid((unsigned)L.ntiles, channels);
     hipLaunchKernelGGL((decim_tile<KV, M, P>), grid, dim3(kDtBlock), smem, s, L);
     return SRCDSP_OK;
@@ -171,8 +171,12 @@ int launch_decim_tile_m(const DecimLaunch &L, int channels, unsigned M, hipStrea
     switch (M) {
     case 1: return launch_decim_tile<KV, 1, P>(L, channels, s);
     case 2: return launch_decim_tile<KV, 2, P>(L, channels, s);
+    case 3: return launch_decim_tile<KV, 3, P>(L, channels, s);
     case 4: return launch_decim_tile<KV, 4, P>(L, channels, s);
-    default: return launch_decim_tile<KV, 8, P>(L, channels, s);
+    case 5: return launch_decim_tile<KV, 5, P>(L, channels, s);
+    case 6: return launch_decim_tile<KV, 6, P>(L, channels, s);
+    case 8: return launch_decim_tile<KV, 8, P>(L, channels, s);
+    default: return launch_decim_tile<KV, 16, P>(L, channels, s);
     }
 }
 
@@ -209,11 +213,11 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
     } else if (f.M == 4 && f.kv == KV_CI16_I32 && f.coef_fits_i24 && al && (f.ntaps == 127 || f.ntaps == 128)) {
         rc = f.ntaps == 127 ? launch_ci16<127>(L, channels, mixed, s) : launch_ci16<128>(L, channels, mixed, s);
     } else if ((f.kv == KV_CF32 || f.kv == KV_CI16_I32 || f.kv == KV_CI16_I16) &&
-               (f.M == 1 || f.M == 2 || f.M == 4 || f.M == 8) &&
+               (f.M <= 6 || f.M == 8 || f.M == 16) &&
                (f.kv == KV_CF32 ? al : aligned8(L.in) && (L.in_stride * 4) % 8 == 0) &&
                (f.kv == KV_CF32 ? out_al : aligned8(L.out) && (L.out_stride * 4) % 8 == 0) &&
                f.ntaps <= kDtMaxTaps && !mixed && L.n_out > 0) {
-        // any tap count <= 1024 at M = 1/2/4/8 (M = 1: FilterFir on complex<int16_t>)
+        // any tap count <= 1024 at M = 1..6, 8, 16 (M = 1: FilterFir on complex<int16_t>)
         if (f.kv == KV_CF32)
             rc = fma ? launch_decim_tile_m<KV_CF32, 1>(L, channels, f.M, s) : launch_decim_tile_m<KV_CF32, 0>(L, channels, f.M, s);
         else if (f.kv == KV_CI16_I16)
@@ -287,9 +291,9 @@ int FirCore::set_coeffs(const void *coeffs, int n, bool keep_history) {
         SRCDSP_HIP_TRY(hipMalloc(&d_cpair, 4 * (size_t)J));
         SRCDSP_HIP_TRY(hipMemcpy(d_cpair, pr.data(), 4 * (size_t)J, hipMemcpyHostToDevice));
     }
-    // 16 zero taps of slack: the tap chunks of decim_tile_cf32 end on 16-tap
+    // 32 zero taps of slack: the tap chunks of decim_tile end on 12/16/20-tap
     // boundaries (taps past N are never applied, but their s_load stays in bounds)
-    tmp.resize(4 * ((size_t)n + 16), '\0');
+    tmp.resize(4 * ((size_t)n + 32), '\0');
     SRCDSP_HIP_TRY(hipMalloc(&d_coef, tmp.size()));
     SRCDSP_HIP_TRY(hipMemcpy(d_coef, tmp.data(), tmp.size(), hipMemcpyHostToDevice));
 

@@ -688,17 +688,21 @@ __device__ __forceinline__ void mix_dot2(uint32_t w, uint32_t C, int32_t &re, in
 // so the image has the cf32 layout: LDS blocks are 8 granules + one pad
 // granule and the lanes' ds_read_b128 are conflict-free.  One tile per
 // workgroup; the image holds ceil(N/16) halo blocks before the tile.
-constexpr int kDtBlock = 256, kDtRM = 16, kDtMaxTaps = 1024;
-constexpr int kDtBS = kDtRM / 2 + 1;  // LDS granules per block (pad included)
+constexpr int kDtBlock = 256, kDtMaxTaps = 1024;
+// samples per lane block: a multiple of M and of 4 (an even number of 16-B
+// granules, so the padded block stride RM/2 + 1 is odd: conflict-free reads)
+__host__ __device__ constexpr int dt_rm(int M) { return M == 1 ? 8 : (M == 3 || M == 6 ? 12 : (M == 5 ? 20 : 16)); }
+__host__ __device__ constexpr int dt_bs(int M) { return dt_rm(M) / 2 + 1; }  // LDS granules per block
 
 template <int KV, int M, int P>
 __global__ __launch_bounds__(kDtBlock) void decim_tile(DecimLaunch a) {
-    static_assert(kDtRM % M == 0, "M divides the block");
+    constexpr int RM = dt_rm(M), BS = dt_bs(M);
+    static_assert(RM % M == 0 && RM % 4 == 0, "block geometry");
     static_assert(KV == KV_CF32 || KV == KV_CI16_I32 || KV == KV_CI16_I16, "sample kinds");
     constexpr bool CF = KV == KV_CF32;
     typedef typename std::conditional<CF, float2, int2>::type X2;
     typedef typename std::conditional<CF, float2, uint32_t>::type SIn;
-    constexpr int R = kDtRM / M, RM = kDtRM, TO = kDtBlock * R;
+    constexpr int R = RM / M, TO = kDtBlock * R;
     extern __shared__ float4 dimg[];
     const int ch = blockIdx.y;
     const SIn *in = (const SIn *)a.in + ch * a.in_stride;
@@ -712,7 +716,7 @@ __global__ __launch_bounds__(kDtBlock) void decim_tile(DecimLaunch a) {
     // image block i holds samples s0 + 16 i .. s0 + 16 i + 15, as (re, im) pairs
     const long s0 = tile * (long)TO * M - (long)NCH * RM;
     const int NG = (NCH + kDtBlock) * (RM / 2);  // 2-sample granules
-    auto put = [&](int g, float4 v) { dimg[(g / (RM / 2)) * kDtBS + g % (RM / 2)] = v; };
+    auto put = [&](int g, float4 v) { dimg[(g / (RM / 2)) * BS + g % (RM / 2)] = v; };
     auto split = [&](uint32_t w0, uint32_t w1) {
         return make_float4(__int_as_float(sext16(w0)), __int_as_float(sext16_hi(w0)), __int_as_float(sext16(w1)),
                            __int_as_float(sext16_hi(w1)));
@@ -765,7 +769,7 @@ __global__ __launch_bounds__(kDtBlock) void decim_tile(DecimLaunch a) {
     auto load = [&](X2 (&w)[RM], int blk) {
 #pragma unroll
         for (int i = 0; i < RM / 2; ++i) {
-            const float4 v = dimg[blk * kDtBS + i];
+            const float4 v = dimg[blk * BS + i];
             if constexpr (CF) {
                 w[2 * i] = make_float2(v.x, v.y);
                 w[2 * i + 1] = make_float2(v.z, v.w);
@@ -823,9 +827,9 @@ __global__ __launch_bounds__(kDtBlock) void decim_tile(DecimLaunch a) {
     const long o0 = tile * TO + (long)t * R;
     if constexpr (CF) {
         float2 *out = (float2 *)a.out + ch * a.out_stride;
-        if (o0 + R <= a.n_out) {
+        if (R % 2 == 0 && o0 + R <= a.n_out) {
 #pragma unroll
-            for (int r = 0; r < R; r += 2)
+            for (int r = 0; r + 1 < R; r += 2)
                 *(float4 *)(out + o0 + r) = make_float4(q16f(yr[r], a.shift), q16f(yi[r], a.shift),
                                                         q16f(yr[r + 1], a.shift), q16f(yi[r + 1], a.shift));
         } else {
@@ -838,9 +842,9 @@ __global__ __launch_bounds__(kDtBlock) void decim_tile(DecimLaunch a) {
         uint32_t w[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) w[r] = pack16(limit16((int32_t)yr[r], a.shift), limit16((int32_t)yi[r], a.shift));
-        if (o0 + R <= a.n_out) {
+        if (R % 2 == 0 && o0 + R <= a.n_out) {
 #pragma unroll
-            for (int r = 0; r < R; r += 2) *(uint2 *)(out + o0 + r) = make_uint2(w[r], w[r + 1]);
+            for (int r = 0; r + 1 < R; r += 2) *(uint2 *)(out + o0 + r) = make_uint2(w[r], w[r + 1]);
         } else {
 #pragma unroll
             for (int r = 0; r < R; ++r)

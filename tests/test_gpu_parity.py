@@ -81,7 +81,9 @@ def test_decim_cf32_tile_kernel_vs_oracle(S, O, fp, ntaps):
 
 @pytest.mark.parametrize("fp", ["fma", "strict"])
 @pytest.mark.parametrize("M,ntaps", [(2, 1), (2, 16), (2, 17), (2, 63), (2, 128), (4, 2), (4, 15), (4, 48),
-                                     (4, 63), (4, 255), (4, 1024), (8, 8), (8, 49), (8, 255), (8, 1000)])
+                                     (4, 63), (4, 255), (4, 1024), (8, 8), (8, 49), (8, 255), (8, 1000),
+                                     (3, 1), (3, 13), (3, 95), (5, 21), (5, 100), (6, 11), (6, 72), (16, 17),
+                                     (16, 256)])
 def test_decim_cf32_any_taps_tile_vs_oracle(S, O, fp, M, ntaps):
     """decim_tile_cf32 (M in 2/4/8, runtime tap count <= 1024): tail tiles,
     calls shorter than the filter, chained uneven calls, both float contracts."""
@@ -98,7 +100,7 @@ def test_decim_cf32_any_taps_tile_vs_oracle(S, O, fp, M, ntaps):
 
 @pytest.mark.parametrize("kind", ["i16", "i24", "i32", "t16"])
 @pytest.mark.parametrize("M,ntaps", [(2, 1), (2, 33), (2, 127), (4, 17), (4, 63), (4, 200), (8, 16), (8, 255),
-                                     (8, 1024)])
+                                     (8, 1024), (3, 40), (5, 61), (6, 13), (16, 100)])
 def test_decim_ci16_any_taps_tile_vs_oracle(S, O, kind, M, ntaps):
     """decim_tile for complex<int16_t> (M in 2/4/8, runtime tap count <= 1024):
     int32 taps in int16 / i24 / wider range (v_mad_i32_i24 or full 32-bit
