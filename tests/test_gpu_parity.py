@@ -244,19 +244,23 @@ def test_fir_float_tile_kernel_vs_oracle(S, O, fp, ntaps):
             assert np.array_equal(g.step(dev(xs)).cpu().numpy(), r.step(xs)), (kind, off, n)
 
 
-def test_decim_batched_equals_single(S, O):
+@pytest.mark.parametrize("M,ntaps", [(4, 127), (2, 63), (8, 200), (3, 50)])
+def test_decim_batched_equals_single(S, O, M, ntaps):
+    """The batched launch (grid.y = channel, configs[2]'s layout) on the headline
+    kernel and on the any-tap tile kernel: per-channel history across steps."""
     import torch
     from srcdsp_amd.design import hamming_sinc
-    c = hamming_sinc(127)
-    C, L = 8, 1 << 16
+    c = hamming_sinc(ntaps)
+    C, L = 8, 3 * (1 << 15)
+    L -= L % M
     x = np.stack([O["fma"].gen_cf32(0x5EED, ch, 0, L) for ch in range(C)])
-    fs = [S.FilterDnsamplingFir(c, 4) for _ in range(C)]
+    fs = [S.FilterDnsamplingFir(c, M) for _ in range(C)]
     xd = dev(x)
     for rep in range(2):  # two steps: history per channel
-        out = torch.empty((C, L // 4), dtype=torch.complex64, device="cuda")
+        out = torch.empty((C, L // M), dtype=torch.complex64, device="cuda")
         S.decim_step_batched(fs, xd, out)
         if rep == 0:
-            refs = [O["fma"].decim(0, 4, c) for _ in range(C)]
+            refs = [O["fma"].decim(0, M, c) for _ in range(C)]
         for ch in range(C):
             assert np.array_equal(out[ch].cpu().numpy(), refs[ch].step(x[ch])), (rep, ch)
 
