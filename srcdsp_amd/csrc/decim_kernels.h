@@ -691,7 +691,7 @@ __device__ __forceinline__ void mix_dot2(uint32_t w, uint32_t C, int32_t &re, in
 constexpr int kDtBlock = 256, kDtMaxTaps = 1024;
 // samples per lane block: a multiple of M and of 4 (an even number of 16-B
 // granules, so the padded block stride RM/2 + 1 is odd: conflict-free reads)
-__host__ __device__ constexpr int dt_rm(int M) { return M == 1 ? 8 : (M == 3 || M == 6 ? 12 : (M == 5 ? 20 : 16)); }
+__host__ __device__ constexpr int dt_rm(int M) { return M <= 2 || M == 4 ? 8 : (M == 3 || M == 6 ? 12 : (M == 5 ? 20 : 16)); }
 __host__ __device__ constexpr int dt_bs(int M) { return dt_rm(M) / 2 + 1; }  // LDS granules per block
 
 template <int KV, int M, int P>
