@@ -1204,8 +1204,21 @@ __global__ __launch_bounds__(kFirBlock) void fir_tile_f32(DecimLaunch a) {
     const long o0 = (long)blockIdx.x * TO;  // first output (= input sample) of the tile
     const int span = TO + P0;                // staged samples, origin o0 - P0
     auto slot = [&](int g) { return g + g / GPL; };
-    // stage: granule-wise, through the cache (halo from history on tile 0)
-    for (int g = t; g < span / SPG; g += BLOCK) {
+    // stage through the cache: the tile's own TO samples with every load of a
+    // lane in flight before the LDS writes (every tile but the launch's last
+    // lies inside the input), then the halo (from history on tile 0) and any
+    // partial tile granule-wise
+    const int GH = P0 / SPG;
+    constexpr int GPB = TO / SPG / BLOCK;  // body granules per lane
+    const bool body_in = o0 + TO <= n_in;
+    if (body_in) {
+        float4 v[GPB];
+#pragma unroll
+        for (int i = 0; i < GPB; ++i) v[i] = *(const float4 *)(in + o0 + (long)(t + i * BLOCK) * SPG);
+#pragma unroll
+        for (int i = 0; i < GPB; ++i) fl[slot(GH + t + i * BLOCK)] = v[i];
+    }
+    for (int g = t; g < (body_in ? GH : span / SPG); g += BLOCK) {
         const long s0 = o0 - P0 + (long)g * SPG;
         float4 v;
         if (s0 >= 0 && s0 + SPG <= n_in) {
