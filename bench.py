@@ -60,7 +60,54 @@ def parse():
     p.add_argument("--no-pcie", action="store_true", help="skip the host-vector (PCIe-inclusive) side measurement")
     p.add_argument("--dump-steps", action="store_true", help="print every timed step's kernel ms to stderr")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    p.add_argument("--dry-run", action="store_true",
+                   help="start the ranks, rendezvous over gloo, print each rank's view of the world, exit "
+                        "before any GPU call (tests the launcher on a CPU host)")
     return p.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args) -> int | None:
+    """`bench.py --gpus N` (N > 1) run without a launcher: start N ranks of
+    this script under torch.distributed.run as a CHILD process (one rank per
+    GPU, rendezvous on 127.0.0.1) and return its exit code.  Called before
+    torch, srcdsp_amd or the GPU is touched; the parent never execs.  Rank 0's
+    JSON line reaches our stdout through the inherited file descriptors.
+    Returns None when this process is itself a rank (WORLD_SIZE set by a
+    launcher) or N == 1."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
+    print(f"bench: starting {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.run(cmd).returncode
+
+
+def dry_run(args) -> None:
+    """One line per rank: the rank/world the launcher gave it and the world a
+    gloo process group actually assembled (an all-reduce of ones).  No GPU."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    seen = 1
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        seen = int(t.item())
+        dist.destroy_process_group()
+    print(json.dumps({"dry_run": True, "rank": rank, "world": world, "world_seen": seen, "gpus": args.gpus}),
+          flush=True)
+    if world != args.gpus or seen != args.gpus:
+        raise SystemExit(f"bench: rank {rank} sees world {world}/{seen}, --gpus {args.gpus}")
 
 
 # "nccl" (= RCCL over xGMI) on a multi-GPU node.  SRCDSP_BENCH_BACKEND=gloo is
@@ -133,6 +180,9 @@ class DecimWorkload(Workload):
 class MixDecimWorkload(Workload):
     dtype = "i32"
     bytes_per_sample = 5.0  # 4 B complex<int16_t> read + 4 B out per 4 inputs
+    # 127 taps -> 64 int16 tap pairs x 2 components per output, 1 output per 4
+    # inputs: 32 v_dot2 lane-ops per input sample (the mixer's own ~9 ops not counted)
+    dot2_per_sample = 32.0
 
     def __init__(self, S, torch, L, channels, rank, fp):
         from srcdsp_amd.design import hamming_sinc, q14
@@ -208,6 +258,9 @@ class UpWorkload(Workload):
     128-tap Q14 interpolator, L = 4, input length L samples -> 4L outputs."""
     dtype = "i32"
     bytes_per_sample = 20.0  # 4 B complex<int16_t> in, 4 x 4 B out per input sample
+    # 4 outputs per input, 32 taps each, 2 components: 256 int MACs = 128 v_dot2
+    # lane-ops per input sample (algorithmic; the kernel issues 136)
+    dot2_per_sample = 128.0
 
     def __init__(self, S, torch, L, channels, rank, fp):
         from srcdsp_amd.design import hamming_sinc, q14
@@ -355,9 +408,27 @@ def cpu_baseline(args):
                       f"{secs:.2f} s; {src}; host CPU: {cpu}"}
 
 
-def cpu_baseline_allcores(args, threads=16):
+def host_cores():
+    """(cores this process may use, description).  SURVEY §8d asks for "all the
+    nproc cores"; on a shared GPU box nproc/os.cpu_count() report the whole
+    machine while this job's share is the affinity mask, further capped by the
+    box's OMP_NUM_THREADS (the per-GPU CPU share, 16 on the MI355X pool)."""
+    total = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = total
+    omp = os.environ.get("OMP_NUM_THREADS")
+    n = aff
+    if omp and omp.isdigit() and 0 < int(omp) < n:
+        n = int(omp)
+    return n, (f"{n} threads = this job's CPU share (affinity mask {aff} CPUs, OMP_NUM_THREADS={omp}); "
+               f"machine nproc {total}")
+
+
+def cpu_baseline_allcores(args, threads=None):
     """the reference on all the host cores this GPU's share of the box
-    gives (16 threads), one independent channel per thread (config 3's layout):
+    gives (host_cores()), one independent channel per thread (config 3's layout):
     each thread owns a FilterDnsamplingFir object from oracle/_ref/strict and
     steps its own channel; value = all threads' samples / the wall time from the
     common start to the last thread's end.  ctypes drops the GIL for the calls."""
@@ -368,13 +439,17 @@ def cpu_baseline_allcores(args, threads=16):
     path = os.path.join(ROOT, "oracle", "_ref", "strict", "libref_decim_old.so")
     if args.workload != "decim" or not os.path.exists(path):
         return None
+    cores_note = f"{threads} threads (caller-set)"
+    if threads is None:
+        threads, cores_note = host_cores()
     lib = C.CDLL(path)
     lib.ref_decim_create.restype = C.c_void_p
     lib.ref_decim_create.argtypes = [C.c_int, C.c_uint, C.c_void_p, C.c_int]
     lib.ref_decim_step_timed.restype = C.c_double
     lib.ref_decim_step_timed.argtypes = [C.c_void_p, C.c_void_p, C.c_long, C.c_void_p]
     lib.ref_decim_destroy.argtypes = [C.c_void_p]
-    n = min(args.cpu_sample, args.samples) // 2
+    # ~2 s of CPU per thread whatever the thread count (bounded host memory)
+    n = min(args.cpu_sample // 2, args.samples // 2, (16 << 26) // threads)  # <= 8 GiB of input in all
     n -= n % 4
     c = hamming_sinc(127)
     o = pyoracle.Oracle(0)
@@ -402,7 +477,7 @@ def cpu_baseline_allcores(args, threads=16):
     return {"value": round(threads * n / wall / 1e6, 3), "unit": "Msamples/s", "cores": threads, "kind": "reference",
             "sample": f"{threads} threads x {n} samples (channels 0..{threads - 1} of the synthetic workload, one "
                       f"FilterDnsamplingFir per thread), {wall:.2f} s wall; oracle/_ref/strict/libref_decim_old.so; "
-                      f"host CPU: {_cpu_model()}"}
+                      f"host CPU: {_cpu_model()}; {cores_note}"}
 
 
 def _cpu_model():
@@ -489,23 +564,44 @@ def pcie_inclusive(S):
 
 def pmc_traffic(args, work_name, per_launch_samples):
     """Per-launch HBM bytes from the committed rocprofv3 PMC summary (see
-    profiles/README.md for how it is collected and corrected), if it matches."""
+    profiles/README.md for how it is collected and corrected), if it was
+    measured on this launch size AND on the current kernel sources (its
+    `kernel_sources_sha` against srcdsp_amd.build.source_digest()).  Returns
+    (bytes or None, note)."""
+    from srcdsp_amd.build import source_digest
     try:
         with open(args.traffic_json) as f:
             t = json.load(f)
-        e = t.get(work_name)
-        if e and int(e.get("samples_per_launch", -1)) == per_launch_samples:
-            return e.get("hbm_bytes_per_launch")
     except Exception:
-        pass
-    return None
+        return None, "no PMC summary"
+    e = t.get(work_name)
+    if not e or int(e.get("samples_per_launch", -1)) != per_launch_samples:
+        return None, "no PMC summary for this workload size"
+    if e.get("kernel_sources_sha") != source_digest():
+        print(f"bench: WARNING {args.traffic_json} entry {work_name} predates the current kernel sources; "
+              "traffic not reported (re-run scripts/pmc_traffic.py)", file=sys.stderr, flush=True)
+        return None, "stale: PMC summary predates the current kernel sources"
+    return e.get("hbm_bytes_per_launch"), "rocprofv3 PMC, " + e.get("correction", "")
 
 
 # ---------------------------------------------------------------- main
 def main():
     args = parse()
+    rc = spawn_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
+    if args.dry_run:
+        dry_run(args)
+        return
     import torch
     world, rank, local = dist_setup(args)
+    reported = world
+    if world > 1:
+        import torch.distributed as dist
+        reported = dist.get_world_size()  # what the process group (RCCL) actually assembled
+    if world != args.gpus or reported != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but the launcher started {world} rank(s) "
+                         f"(process group: {reported})")
     import srcdsp_amd as S
     from srcdsp_amd.dist import gather_to_root, max_over_ranks
     S.lib()  # loud failure if the HIP library is missing
@@ -539,6 +635,12 @@ def main():
     if args.workload in ("up", "fifo", "iq"):
         units_per_rank = work.n * args.steps
     total_samples = units_per_rank * world
+    if args.workload == "corr":
+        # the reference's step() stops at the first detection (correlators.h:296
+        # `break`): the samples it processes are those up to and including the
+        # one after the peak, not the whole buffer
+        found, idx = work.last
+        total_samples = ((idx + 2) if found else L) * args.steps
     value = total_samples / wall / 1e6
     ms_per_step = wall / args.steps * 1e3
 
@@ -556,8 +658,9 @@ def main():
     if args.workload in ("up", "fifo", "iq"):
         per_launch_samples = work.n
     achieved = work.bytes_per_sample * per_launch_samples / (kern_avg_ms * 1e-3) / 1e9
+    traffic, traffic_note = pmc_traffic(args, work.name, per_launch_samples)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args, work.name, per_launch_samples),
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_note,
             "kernel": work.name, "kernel_ms": round(kern_avg_ms, 4),
             "algorithmic_bytes_per_launch": int(work.bytes_per_sample * per_launch_samples)}
     if getattr(work, "bound", "hbm") == "pcie":
@@ -567,6 +670,19 @@ def main():
         roof = {"bound": "pcie", "achieved": round(gbs, 2), "peak": PCIE_PEAK_GBS, "unit": "GB/s",
                 "frac": round(gbs / PCIE_PEAK_GBS, 4), "traffic": None, "kernel": work.name,
                 "kernel_ms": round(kern_avg_ms, 4), "note": "whole step on the consumer stream (host -> HBM -> chain)"}
+    dps = getattr(work, "dot2_per_sample", None)
+    if dps:
+        # integer kernels on v_dot2: the VALU roofline beside the HBM one; the
+        # binding resource (higher fraction) is `roofline`, the other rides along
+        tops = dps * per_launch_samples / (kern_avg_ms * 1e-3) / 1e12
+        valu = {"bound": "valu", "achieved": round(tops, 2), "peak": VALU_PEAK_TOPS, "unit": "T v_dot2 lane-ops/s",
+                "frac": round(tops / VALU_PEAK_TOPS, 4), "traffic": None, "kernel": work.name,
+                "kernel_ms": round(kern_avg_ms, 4), "dot2_per_input_sample": dps}
+        if valu["frac"] > roof["frac"]:
+            roof, other = valu, roof
+        else:
+            other = valu
+        roof = dict(roof, other_bound=other)
     if args.workload == "corr":
         # VALU-bound: 1024 complex taps = 4096 int MACs =
         # 2048 v_dot2 lane-ops per scanned sample; the reference scans up to and
@@ -597,7 +713,8 @@ def main():
                 "scaling": "strong" if args.workload == "corr" and world > 1 else "weak",
                 "vs_baseline": None, "dtype": work.dtype,
                 "data": "synthetic (counter-based splitmix64 integer samples, SURVEY §8d)", "config": cfg,
-                "roofline": roof}
+                "roofline": roof, "world_size_reported": reported,
+                "backend": BACKEND if world > 1 else None}
         if gather_ms is not None:
             line["gather_ms"] = round(gather_ms, 3)
             line["gather_bytes"] = int(world * work.y.numel() * work.y.element_size())

@@ -256,6 +256,67 @@ SRCDSP_API int srcdsp_iq_load(const char *path, size_t component_bytes, void *d_
                               void *stream);
 SRCDSP_API int srcdsp_iq_load_host(const char *path, size_t component_bytes, void *out, size_t cap, size_t *n);
 
+/* ============================================================================
+ * Multi-GPU (BASELINE configs[2]): one host process drives
+ * several GPUs of one node.  The reference has no multi-device code; these
+ * entries shard what its users do with one FilterDnsamplingFir object per
+ * channel (dnsampling_filters.h:49-172) across devices, and bring the results
+ * back with RCCL over xGMI.
+ *
+ * srcdsp_comm_t: one RCCL communicator per device, made together in this
+ * process by ncclCommInitAll (rccl.h:236), plus one non-blocking HIP stream
+ * per device on which the sharded operators run.  `rank` below = index into
+ * the device list.
+ * ==========================================================================*/
+typedef struct srcdsp_comm *srcdsp_comm_t;
+/* devs may be NULL (devices 0..ndev-1) */
+SRCDSP_API int srcdsp_comm_create(srcdsp_comm_t *out, int ndev, const int *devs);
+SRCDSP_API int srcdsp_comm_destroy(srcdsp_comm_t c);
+/* ndev, and the HIP device id of each rank (devs may be NULL) */
+SRCDSP_API int srcdsp_comm_info(srcdsp_comm_t c, int *ndev, int *devs);
+/* the hipStream_t (as void*) the sharded operators use on rank's device */
+SRCDSP_API int srcdsp_comm_stream(srcdsp_comm_t c, int rank, void **stream);
+/* wait for every rank's stream */
+SRCDSP_API int srcdsp_comm_synchronize(srcdsp_comm_t c);
+
+/* `channels` independent FilterDnsamplingFir objects of one configuration
+ * (same variant/M/taps/flags as srcdsp_decim_create), block-partitioned over
+ * the comm's devices: rank r owns channels [first_r, first_r + count_r), the
+ * first channels % ndev ranks one more.  Each channel keeps its own history
+ * on its own device; a step is one batched launch per device (no collective). */
+typedef struct srcdsp_decim_sharded *srcdsp_decim_sharded_t;
+SRCDSP_API int srcdsp_decim_sharded_create(srcdsp_decim_sharded_t *out, srcdsp_comm_t comm, int channels,
+                                           int variant, unsigned M, const void *coeffs, int ntaps,
+                                           unsigned flags);
+SRCDSP_API int srcdsp_decim_sharded_destroy(srcdsp_decim_sharded_t h);
+SRCDSP_API int srcdsp_decim_sharded_partition(srcdsp_decim_sharded_t h, int rank, int *first_channel,
+                                              int *count);
+/* the per-channel handle of global channel ch (for reset / setCoeffs /
+ * setLeftShiftBy2 / get_state on its own device) */
+SRCDSP_API int srcdsp_decim_sharded_channel(srcdsp_decim_sharded_t h, int ch, srcdsp_decim_t *handle);
+/* one step() of every channel: d_in[r] / d_out[r] are device pointers on
+ * rank r's device holding its count_r channels as rows in_stride / out_stride
+ * samples apart; n_in samples per channel (n_in % M == 0).  Asynchronous on
+ * the comm streams. */
+SRCDSP_API int srcdsp_decim_sharded_step(srcdsp_decim_sharded_t h, const void *const *d_in, size_t in_stride,
+                                         void *const *d_out, size_t out_stride, size_t n_in);
+/* reset every channel (dnsampling_filters.h:56-60), each on its own device */
+SRCDSP_API int srcdsp_decim_sharded_reset(srcdsp_decim_sharded_t h);
+/* host std::vector convenience (reference-style: one vector per channel):
+ * in[ch] -> out[ch] for every channel, n_in samples each; each device's
+ * channels staged through pinned memory by one host thread per device;
+ * returns when every output is on the host. */
+SRCDSP_API int srcdsp_decim_sharded_step_host(srcdsp_decim_sharded_t h, const void *const *in, void *const *out,
+                                              size_t n_in);
+/* result gather to one device: channel ch's n_out outputs land at
+ * d_root + ch*n_out samples (d_root on rank `root`'s device, room for
+ * channels*n_out samples).  ncclGather (rccl.h:745) when every rank holds the
+ * same number of contiguous rows, else grouped ncclSend/ncclRecv
+ * (rccl.h:700,720) with the root's own rows copied on its device.
+ * Asynchronous on the comm streams. */
+SRCDSP_API int srcdsp_decim_sharded_gather(srcdsp_decim_sharded_t h, void *const *d_out, size_t out_stride,
+                                           size_t n_out, void *d_root, int root);
+
 /* ---------------------------------------------------------------- misc */
 /* Last error text of the calling thread (HIP error string or argument check). */
 SRCDSP_API const char *srcdsp_last_error(void);

@@ -9,8 +9,8 @@ for w in decim corr; do
   extra=""
   [ $w = corr ] && extra="--samples 16777216 --steps 2 --warmup 1"
   [ $w = decim ] && extra="--samples 67108864 --steps 3 --warmup 1"
-  timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-      --master-port 29511 bench.py --gpus 2 --workload $w --no-cpu-baseline $extra \
+  # bench.py --gpus 2 starts its own 2 ranks (a child torch.distributed.run)
+  timeout -k 10 400 python bench.py --gpus 2 --workload $w --no-cpu-baseline $extra \
       > gpurun_out/dist_${w}.log 2>&1 || { echo "[dist_$w] failed"; exit 1; }
   echo "[dist_$w] ok"
 done

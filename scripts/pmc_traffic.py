@@ -21,6 +21,8 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from srcdsp_amd.build import source_digest  # noqa: E402
 KERNEL_KEYS = {"decim": "decim_stream2_cf32", "mixdecim": "decim_dot2_ci16", "corr": "corr_eval",
                "fir": "fir_stream_f32", "up": "up_tile"}
 BYTES_PER_SAMPLE = {"decim": 10.0, "mixdecim": 5.0, "corr": 4.0, "fir": 12.0, "up": 20.0}
@@ -81,7 +83,8 @@ def main():
              "read_bytes_per_launch": int(read_b), "write_bytes_per_launch": int(write_b),
              "algorithmic_bytes_per_launch": int(alg), "traffic_over_algorithmic": (read_b + write_b) / alg,
              "raw_counters_per_launch": res,
-             "correction": "read = 2*FETCH_SIZE*1024 (gfx950 half-count), write = WRITE_SIZE*1024"}
+             "correction": "read = 2*FETCH_SIZE*1024 (gfx950 half-count), write = WRITE_SIZE*1024",
+             "kernel_sources_sha": source_digest()}
     if "SQ_WAVE_CYCLES" in res and res.get("SQ_WAVE_CYCLES"):
         entry["valu_active_frac_of_wave_cycles"] = res["SQ_ACTIVE_INST_VALU"] / res["SQ_WAVE_CYCLES"]
         entry["wait_any_frac"] = res["SQ_WAIT_ANY"] / res["SQ_WAVE_CYCLES"]

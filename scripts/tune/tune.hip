@@ -190,3 +190,30 @@ extern "C" int tune_fir(int variant, int grid, const float *d_coef, const void *
     }
     return -1;
 }
+
+// ---- clock probe (tuning only): one lane records (s_memtime, s_memrealtime)
+// every `gap` ticks of the 100 MHz real-time counter, n times, while other
+// kernels run beside it on another stream; d(memtime)/d(realtime) x 100 MHz is
+// the shader clock the chip holds at that moment (MI355X_MICROARCH.md, DVFS).
+__global__ void clock_probe(unsigned long long *out, int n, int gap) {
+    if (threadIdx.x != 0) return;
+    for (int i = 0; i < n; ++i) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)gap) __builtin_amdgcn_s_sleep(4);
+        const unsigned long long c = __builtin_amdgcn_s_memtime();
+        const unsigned long long r = __builtin_amdgcn_s_memrealtime();
+        out[2 * i] = c;
+        out[2 * i + 1] = r;
+    }
+}
+__global__ void realtime_stamp(unsigned long long *out) {
+    if (threadIdx.x == 0) out[0] = __builtin_amdgcn_s_memrealtime();
+}
+extern "C" int tune_clock_probe(unsigned long long *out, int n, int gap, void *stream) {
+    hipLaunchKernelGGL(clock_probe, dim3(1), dim3(64), 0, (hipStream_t)stream, out, n, gap);
+    return hipGetLastError();
+}
+extern "C" int tune_realtime_stamp(unsigned long long *out, void *stream) {
+    hipLaunchKernelGGL(realtime_stamp, dim3(1), dim3(64), 0, (hipStream_t)stream, out);
+    return hipGetLastError();
+}

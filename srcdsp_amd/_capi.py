@@ -81,6 +81,19 @@ SIGNATURES = {
     "srcdsp_iq_count": (I, [C.c_char_p, SZ, C.POINTER(C.c_size_t)]),
     "srcdsp_iq_load": (I, [C.c_char_p, SZ, VP, SZ, C.POINTER(C.c_size_t), VP]),
     "srcdsp_iq_load_host": (I, [C.c_char_p, SZ, VP, SZ, C.POINTER(C.c_size_t)]),
+    "srcdsp_comm_create": (I, [HP, I, IP]),
+    "srcdsp_comm_destroy": (I, [VP]),
+    "srcdsp_comm_info": (I, [VP, IP, IP]),
+    "srcdsp_comm_stream": (I, [VP, I, HP]),
+    "srcdsp_comm_synchronize": (I, [VP]),
+    "srcdsp_decim_sharded_create": (I, [HP, VP, I, I, U, VP, I, U]),
+    "srcdsp_decim_sharded_destroy": (I, [VP]),
+    "srcdsp_decim_sharded_partition": (I, [VP, I, IP, IP]),
+    "srcdsp_decim_sharded_channel": (I, [VP, I, HP]),
+    "srcdsp_decim_sharded_step": (I, [VP, HP, SZ, HP, SZ, SZ]),
+    "srcdsp_decim_sharded_reset": (I, [VP]),
+    "srcdsp_decim_sharded_step_host": (I, [VP, HP, HP, SZ]),
+    "srcdsp_decim_sharded_gather": (I, [VP, HP, SZ, SZ, VP, I]),
     "srcdsp_last_error": (C.c_char_p, []),
     "srcdsp_version": (C.c_char_p, []),
     "srcdsp_fill_synthetic": (I, [VP, I, SZ, U64, U64, U64, I, I, VP]),

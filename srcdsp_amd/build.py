@@ -20,6 +20,7 @@ OBJ = os.path.join(ROOT, "build", "srcdsp_hip")
 LIB_DIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIB_DIR, "libsrcdsp_hip.so")
 ARCH = os.environ.get("SRCDSP_OFFLOAD_ARCH", "gfx950")
+ROCM_LIB = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib")
 
 CXXFLAGS = [
     f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden",
@@ -39,6 +40,19 @@ def _hipcc() -> str:
 
 def _headers() -> list[str]:
     return glob.glob(os.path.join(CSRC, "*.h")) + [os.path.join(ROOT, "include", "srcdsp_hip.h")]
+
+
+def source_digest() -> str:
+    """sha256 (16 hex) over the kernel sources (csrc/*.hip, csrc/*.h and the C
+    ABI header): stamps measured evidence (profiles/pmc_traffic.json) with the
+    code it was measured on, so a later kernel change shows it as stale."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in sorted(glob.glob(os.path.join(CSRC, "*.hip")) + _headers()):
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def _stale(target: str, deps: list[str]) -> bool:
@@ -69,7 +83,9 @@ def build(verbose: bool = False, jobs: int = 8) -> str:
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(compile_one, srcs))
     if _stale(LIB, objs):
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
+        # RCCL for the multi-GPU entries (multi.hip: ncclCommInitAll, ncclGather, ncclSend/Recv)
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs,
+               f"-L{ROCM_LIB}", "-lrccl", f"-Wl,-rpath,{ROCM_LIB}"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         r = subprocess.run(cmd, capture_output=True, text=True)

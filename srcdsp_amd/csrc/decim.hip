@@ -95,15 +95,21 @@ int launch_ci16(DecimLaunch L, int channels, bool mixed, hipStream_t s) {
     return SRCDSP_OK;
 }
 
-// dot2 ci16 kernel shape: tile lanes and mixer table form.  SRCDSP_CI16_VARIANT
-// (tuning only) selects 0: 256 lanes, 1: 512 lanes, 2: 256 lanes + doubled
+// dot2 ci16 kernel shape: tile lanes and mixer table form.  The product ships
+// one shape (512 lanes, doubled mixer table: measured best, profiles/); a
+// tuning build (-DSRCDSP_TUNING, scripts/tune) can pick another with
+// SRCDSP_CI16_VARIANT = 0: 256 lanes, 1: 512 lanes, 2: 256 lanes + doubled
 // table, 3: 512 lanes + doubled table.
 static int ci16_variant() {
+#ifdef SRCDSP_TUNING
     static const int v = [] {
         const char *e = std::getenv("SRCDSP_CI16_VARIANT");
         return e ? std::atoi(e) : 3;
     }();
     return v;
+#else
+    return 3;
+#endif
 }
 
 template <int NT, int BLOCK, bool TAB2>

@@ -331,6 +331,45 @@ def test_headline_size_properties(S, O):
     torch.cuda.empty_cache()
 
 
+def test_config3_per_gpu_share_size_properties(S, O):
+    """Config 3's per-GPU share at full size: 8 channels x 2^28 complex<float>
+    samples (channels 8..15 of the 64, i.e. rank 1 of 8), one batched launch
+    (grid.y = channel), as bench.py --gpus N steps it.  Spot windows of every
+    channel (first tiles, tile seams, random interior, last tile) against the
+    oracle on the same input windows; the device generator is checked against
+    the host one on each window."""
+    import torch
+    from srcdsp_amd.design import hamming_sinc
+    c = hamming_sinc(127)
+    C, L = 8, 1 << 28
+    ch0 = 8
+    x = torch.empty((C, L), dtype=torch.complex64, device="cuda")
+    for k in range(C):
+        S.fill_synthetic(x[k], "cf32", seed=0x5EED, channel=ch0 + k)
+    y = torch.empty((C, L // 4), dtype=torch.complex64, device="cuda")
+    fs = [S.FilterDnsamplingFir(c, 4, fp="fma") for _ in range(C)]
+    S.decim_step_batched(fs, x, y)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(3)
+    n_out = L // 4
+    for k in range(C):
+        starts = [0, 2048 - 3, n_out - 1000] + list(rng.integers(40, n_out - 1000, 3))
+        for s0 in starts:
+            s0 = int(s0)
+            lo = max(0, 4 * s0 - 128)
+            xin = x[k, lo:4 * (s0 + 64)].cpu().numpy()
+            assert np.array_equal(xin, O["fma"].gen_cf32(0x5EED, ch0 + k, lo, len(xin))), (k, s0)
+            r = O["fma"].decim(0, 4, c).step(xin)[(4 * s0 - lo) // 4:]
+            got = y[k, s0:s0 + 64].cpu().numpy()
+            assert np.array_equal(got, r[:len(got)]), (k, s0)
+    # the channels are independent objects: their histories are their own tails
+    for k in (0, C - 1):
+        h = fs[k].state()["history"]
+        assert h.tobytes() == x[k, L - 126:].cpu().numpy().tobytes(), k
+    del x, y
+    torch.cuda.empty_cache()
+
+
 def test_config4_size_properties(S, O):
     """Config 4 at full size (2^28 complex<int16_t>, device-resident, one fused
     mixer -> decimator step): output windows (first tile, tile seams, random
