@@ -61,7 +61,7 @@ def main():
         elif var == "copy":
             lib.tune_stream_probe2(0, 8192, C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), L, st)
         else:
-            lib.tune_decim(int(var), 1024, C.c_void_p(cdev.data_ptr()), C.c_void_p(x.data_ptr()),
+            lib.tune_decim(int(var), int(os.environ.get("RAMP_GRID", "1024")), C.c_void_p(cdev.data_ptr()), C.c_void_p(x.data_ptr()),
                            C.c_void_p(y.data_ptr()), L, C.c_void_p(h0.data_ptr()), C.c_void_p(h1.data_ptr()), st)
 
     lib.tune_clock_probe(C.c_void_p(stamps.data_ptr()), nst, gap, C.c_void_p(side.cuda_stream))

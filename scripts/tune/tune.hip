@@ -2,6 +2,7 @@
 // variants from srcdsp_amd/csrc/decim_kernels.h and an FMA-rate microbenchmark
 // so they can be timed side by side, interleaved, in one process.
 #include "../../srcdsp_amd/csrc/decim_kernels.h"
+#include "decim_mfma.h"
 
 using namespace srcdsp;
 
@@ -156,6 +157,18 @@ extern "C" int tune_decim(int variant, int grid, const float *d_coef, const void
     case 122: L.ntiles = tiles(512 * 8); return launch(decim_stream2_cf32<127, 8, 512, true, 2, true, 0, true, true, true, true>, grid, 512, L, s);
     case 123: L.ntiles = tiles(128 * 8); return launch(decim_stream2_cf32<127, 8, 128, true, 2, true, 0, true, true, true, true>, grid, 128, L, s);
     // OST 2: permlane32-paired whole-line stores (no LDS output staging, 2 barriers per tile)
+    // matrix-core decimator (decim_mfma.h): 1024-output tiles, 2 workgroups per CU
+    case 300: L.ntiles = tiles(1024); return launch(decim_mfma_cf32<127, 2, true, 0>, grid, 256, L, s);
+    case 301: L.ntiles = tiles(1024); return launch(decim_mfma_cf32<127, 2, true, 2>, grid, 256, L, s);
+    case 302: L.ntiles = tiles(1024); return launch(decim_mfma_cf32<127, 2, true, 1>, grid, 256, L, s);
+    case 303: L.ntiles = tiles(1024); return launch(decim_mfma_cf32<127, 3, true, 0>, grid, 256, L, s);
+    case 304: L.ntiles = tiles(1024); return launch(decim_mfma_cf32<127, 3, true, 2>, grid, 256, L, s);
+    // ILV: tap-major pk_fma issue order (inline asm)
+    case 200: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, 2, true, true, -1, -1, true>, grid, 512, L, s);
+    case 201: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 2, true, 2, true, true, -1, -1, true>, grid, 512, L, s);
+    case 202: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 2, true, 0, true, 2, true, true, -1, -1, true>, grid, 512, L, s);
+    case 203: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 0, true, 2, true, true, -1, -1, true>, grid, 256, L, s);
+    case 204: L.ntiles = tiles(512 * 8); return launch(decim_stream2_cf32<127, 8, 512, true, 2, true, 0, true, 2, true, true, -1, -1, true>, grid, 512, L, s);
     case 70: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, 2, true, true>, grid, 512, L, s);
     case 71: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 1, true, 2, true, true>, grid, 512, L, s);
     case 72: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 2, true, 0, true, 2, true, true>, grid, 512, L, s);
@@ -215,5 +228,19 @@ extern "C" int tune_clock_probe(unsigned long long *out, int n, int gap, void *s
 }
 extern "C" int tune_realtime_stamp(unsigned long long *out, void *stream) {
     hipLaunchKernelGGL(realtime_stamp, dim3(1), dim3(64), 0, (hipStream_t)stream, out);
+    return hipGetLastError();
+}
+
+// ---- layout / numerics probe of v_mfma_f32_4x4x1_16b_f32: K steps of
+// per-lane A and B values (a[k*64 + lane], b[k*64 + lane]) accumulated from 0;
+// D (4 floats per lane) written to d[lane*4 + r]
+__global__ void mfma4x4_probe(const float *a, const float *b, float *d, int K) {
+    const int l = threadIdx.x;
+    f4m_t acc = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < K; ++k) acc = __builtin_amdgcn_mfma_f32_4x4x1f32(a[k * 64 + l], b[k * 64 + l], acc, 0, 0, 0);
+    for (int r = 0; r < 4; ++r) d[l * 4 + r] = acc[r];
+}
+extern "C" int tune_mfma4x4_probe(const float *a, const float *b, float *d, int K, void *stream) {
+    hipLaunchKernelGGL(mfma4x4_probe, dim3(1), dim3(64), 0, (hipStream_t)stream, a, b, d, K);
     return hipGetLastError();
 }

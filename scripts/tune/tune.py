@@ -28,6 +28,7 @@ lib.tune_fma_rate.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
 if lib_old is not None:
     lib_old.tune_decim_old.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_long, C.c_void_p,
                                        C.c_void_p, C.c_void_p]
+lib.tune_mfma4x4_probe.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
 lib.tune_decim.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_long, C.c_void_p,
                            C.c_void_p, C.c_void_p]
 
@@ -114,6 +115,17 @@ def main():
                     (96, 512, "384 mw4 g512"), (93, 256, "768 mw3 g256"), (93, 512, "768 mw3 g512"),
                     (94, 512, "PROBE1 384 mw3 g512"), (95, 256, "PROBE1 768 mw3 g256"), (71, 1024, "PROBE1 head g1024"),
                     (70, 1024, "head (again)")]
+    if os.environ.get("TUNE_ILV"):  # tap-major pk_fma issue order (inline asm) vs the compiler's order
+        variants = [(70, 1024, "head g1024"), (200, 1024, "ILV g1024"), (73, 1024, "PROBE2 head g1024"),
+                    (201, 1024, "PROBE2 ILV g1024"), (202, 512, "ILV mw2 g512"), (202, 256, "ILV mw2 g256"),
+                    (203, 2048, "ILV 256 g2048"), (204, 512, "ILV R8 mw2 g512"), (204, 256, "ILV R8 mw2 g256"),
+                    (71, 1024, "PROBE1 head g1024"), (70, 1024, "head (again)"), (200, 1024, "ILV (again)")]
+    if os.environ.get("TUNE_MFMA"):  # matrix-core decimator (decim_mfma.h) vs the VALU headline
+        variants = [(70, 1024, "head g1024"), (300, 512, "MFMA mw2 g512"), (73, 1024, "PROBE2 head g1024"),
+                    (301, 512, "PROBE2 MFMA g512"), (302, 512, "PROBE1 MFMA g512"), (71, 1024, "PROBE1 head g1024"),
+                    (300, 1024, "MFMA mw2 g1024"), (303, 768, "MFMA mw3 g768"), (304, 768, "PROBE2 MFMA mw3 g768"),
+                    (70, 1024, "head (again)"),
+                    (300, 512, "MFMA (again)")]
     if os.environ.get("TUNE_FIR"):
         fir_ab()
         return
@@ -211,7 +223,12 @@ def sustained_rounds(variants, x, y, cdev, h0, h1, stream, L, ref, rounds=4, rep
         tune_decim(v[0], v[1], C.c_void_p(cdev.data_ptr()), C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()),
                        L, C.c_void_p(h0.data_ptr()), C.c_void_p(h1.data_ptr()), stream)
         torch.cuda.synchronize()
-        assert torch.equal(y.view(torch.int32), ref.view(torch.int32)), v
+        eq = y.view(torch.int32) == ref.view(torch.int32)
+        if not bool(eq.all()):
+            bad = (~eq).nonzero().flatten()
+            print(f"MISMATCH {v[2]}: {bad.numel()} words differ, first {bad[:8].tolist()}", flush=True)
+        else:
+            print(f"bit-exact {v[2]}", flush=True)
     st = torch.cuda.current_stream()
     for rnd in range(rounds):
         for v in variants:

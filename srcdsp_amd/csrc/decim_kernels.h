@@ -6,6 +6,27 @@
 
 namespace srcdsp {
 typedef short short2_t_ __attribute__((ext_vector_type(2)));
+typedef float f2_t __attribute__((ext_vector_type(2)));
+
+// One packed fma step of a complex<float> accumulator by a real tap that sits
+// in one half of an SGPR pair: acc = fma(c, x, acc) per component.  Inline asm
+// so the tap loop issues in the order written (every accumulator's chain
+// advances one tap before any advances the next): the scheduler otherwise
+// groups up to ten dependent v_pk_fma_f32 of one chain back to back, each
+// waiting for the previous one's result.  HI: the tap is the pair's odd
+// element.  ZERO: acc starts from +0 (fma(c, x, +0), as the first step of
+// the reference's accumulation from 0).
+template <bool HI, bool ZERO>
+__device__ __forceinline__ void pk_fma_tap(f2_t &acc, unsigned long long cp, f2_t x) {
+    if constexpr (ZERO && HI)
+        asm volatile("v_pk_fma_f32 %0, %1, %2, 0 op_sel:[1,0,0] op_sel_hi:[1,1,0]" : "=v"(acc) : "s"(cp), "v"(x));
+    else if constexpr (ZERO)
+        asm volatile("v_pk_fma_f32 %0, %1, %2, 0 op_sel_hi:[0,1,0]" : "=v"(acc) : "s"(cp), "v"(x));
+    else if constexpr (HI)
+        asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "s"(cp), "v"(x));
+    else
+        asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[0,1,1]" : "+v"(acc) : "s"(cp), "v"(x));
+}
 
 // ------------------------------------------------------------ arithmetic
 template <bool FMA>
@@ -236,9 +257,13 @@ __device__ __forceinline__ void store_wave_lines(float2 *wo, const float2 (&o)[R
 // second pair with lane i's, so each of the two store instructions writes
 // 1 KiB of whole lines, with no LDS round trip and no barrier.
 template <int NT, int R, int BLOCK, bool FMA, int MINW, bool Q0, int PROBE = 0, bool NTL = false, int OST = 0,
-          bool NTS = false, bool GS = false, int LAUX = -1, int SAUX = -1>
+          bool NTS = false, bool GS = false, int LAUX = -1, int SAUX = -1, bool ILV = false>
 __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a) {
-    static_assert(OST != 2 || R == 4, "the permlane32 store pairing assumes 4 outputs per lane");
+    static_assert(OST != 2 || R == 4 || R == 8, "whole-line stores assume 4 or 8 outputs per lane");
+#ifndef SRCDSP_TUNING
+    // the probe / cache-policy / issue-order variants exist for scripts/tune only
+    static_assert(PROBE == 0 && LAUX < 0 && SAUX < 0 && !ILV, "tuning-only variant: build with -DSRCDSP_TUNING");
+#endif
     constexpr int NQ = (NT + 3) / 4;
     constexpr int TO = BLOCK * R;
     constexpr int TG = 2 * TO + 2 * NQ;
@@ -342,6 +367,34 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
         if constexpr (PROBE == 1) {
 #pragma unroll
             for (int r = 0; r < R; ++r) { yr[r] = X[4 * r + 4 * NQ].x; yi[r] = X[4 * r + 4 * NQ].y; }
+        } else if constexpr (ILV && FMA && PROBE != 3) {
+            // tap-major issue order through pk_fma_tap: R independent chains
+            // round-robin, taps as SGPR pairs (c[2m], c[2m+1])
+            ConstPtr<unsigned long long> tp2 = const_view<unsigned long long>(a.coef);
+            asm volatile("" : "+s"(tp2));
+            f2_t acc[R];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                if (q + 1 < NQ) load_group(-q - 2);
+                if ((q & 3) == 0) asm volatile("" : "+s"(tp2));
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    const int k = 4 * q + p;
+                    if (k < NT) {
+                        const unsigned long long cp = tp2[k >> 1];
+#pragma unroll
+                        for (int r = 0; r < R; ++r) {
+                            const float2 x = X[4 * (r - q) - p + 4 * NQ];
+                            const f2_t xv = {x.x, x.y};
+                            if (k == 0) pk_fma_tap<false, true>(acc[r], cp, xv);
+                            else if (k & 1) pk_fma_tap<true, false>(acc[r], cp, xv);
+                            else pk_fma_tap<false, false>(acc[r], cp, xv);
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r) { yr[r] = acc[r].x; yi[r] = acc[r].y; }
         } else
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
@@ -1088,7 +1141,6 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
 // as 16-B granules with one pad granule after every lane chunk (8 samples),
 // so lanes' ds_read_b128 land on distinct bank slots (odd granule stride).
 constexpr int kFirMaxTaps = 1024;
-typedef float f2_t __attribute__((ext_vector_type(2)));
 constexpr int kFirR = 8, kFirBlock = 256;
 
 template <int KV>
