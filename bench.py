@@ -48,7 +48,7 @@ def parse():
     # is 100 untimed steps before 200 timed ones (~0.15 s of GPU time).
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=100)
-    p.add_argument("--workload", default="decim", choices=["decim", "mixdecim", "corr", "fir", "up", "fifo", "iq"])
+    p.add_argument("--workload", default="decim", choices=["decim", "mixdecim", "ci16decim", "corr", "fir", "up", "fifo", "iq"])
     p.add_argument("--samples", type=int, default=1 << 28, help="input samples per channel per step")
     # default: 1 channel at N=1 (configs[1], the headline); 8 per GPU at N>1,
     # i.e. configs[2]'s 64 independent channels over 8 GPUs, weak-scaled
@@ -276,6 +276,26 @@ class UpWorkload(Workload):
         self.f.step(self.x, self.y)
 
 
+class Ci16DecimWorkload(Workload):
+    """SURVEY §8a row a2 on its own: FilterDnsamplingFir<ci16,ci16,ci32,int32_t,4>,
+    127 Q14 taps, no mixer (config 4's decimator)."""
+    dtype = "i32"
+    bytes_per_sample = 5.0
+    dot2_per_sample = 32.0
+
+    def __init__(self, S, torch, L, channels, rank, fp):
+        from srcdsp_amd.design import hamming_sinc, q14
+        cq = q14(hamming_sinc(127))
+        self.x = torch.empty((L, 2), dtype=torch.int16, device="cuda")
+        S.fill_synthetic(self.x, "ci16", seed=SEED, channel=rank, lo=-8192, hi=8191)
+        self.y = torch.empty((L // 4, 2), dtype=torch.int16, device="cuda")
+        self.d = S.FilterDnsamplingFir(cq, 4, "complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int32_t")
+        self.name = "decim_ci16_q14_m4_t127"
+
+    def step(self):
+        self.d.step(self.x, self.y)
+
+
 def _mixdecim_chain(S):
     """config 4's operators: Mixer<ci16,ci16,int16_t,4096> at f = 0.1 feeding the
     127-tap Q14 FilterDnsamplingFir<ci16,ci16,ci32,int32_t,4>"""
@@ -353,7 +373,7 @@ class IqLoadWorkload(Workload):
             pass
 
 
-WORKLOADS = {"decim": DecimWorkload, "mixdecim": MixDecimWorkload, "corr": CorrWorkload, "fir": FirWorkload,
+WORKLOADS = {"decim": DecimWorkload, "mixdecim": MixDecimWorkload, "ci16decim": Ci16DecimWorkload, "corr": CorrWorkload, "fir": FirWorkload,
              "up": UpWorkload, "fifo": FifoWorkload, "iq": IqLoadWorkload}
 PCIE_PEAK_GBS = 63.0  # MI355X_MICROARCH.md: host link PCIe Gen5 x16, 63 GB/s (spec)
 
@@ -496,7 +516,16 @@ def cpu_baseline_other(args, pyoracle):
         return None
     ref = pyoracle.Reference("strict")
     o = pyoracle.Oracle(0)
-    if args.workload in ("mixdecim", "fifo", "iq"):
+    if args.workload == "ci16decim":
+        n = min(1 << 25, args.samples)
+        n -= n % 4
+        x = o.gen_ci16(SEED, 0, 0, n, -8192, 8191)
+        d = ref.decim(1, 4, q14(hamming_sinc(127)))
+        t0 = time.perf_counter()
+        d.step(x)
+        secs = time.perf_counter() - t0
+        what = "FilterDnsamplingFir<ci16,ci16,ci32,int32_t,4>::step, 127 Q14 taps"
+    elif args.workload in ("mixdecim", "fifo", "iq"):
         n = min(1 << 25, args.samples)
         n -= n % 4
         x = o.gen_ci16(SEED, 0, 0, n, -8192, 8191)
@@ -697,8 +726,8 @@ def main():
 
     if rank == 0:
         cfg = {"workload": work.name, "samples_per_channel": L, "channels_per_gpu": args.channels_per_gpu,
-               "taps": {"decim": 127, "mixdecim": 127, "fir": 31, "up": 128}.get(args.workload),
-               "decimation": {"decim": 4, "mixdecim": 4}.get(args.workload), "interpolation": 4 if args.workload == "up" else None,
+               "taps": {"decim": 127, "mixdecim": 127, "ci16decim": 127, "fir": 31, "up": 128}.get(args.workload),
+               "decimation": {"decim": 4, "mixdecim": 4, "ci16decim": 4}.get(args.workload), "interpolation": 4 if args.workload == "up" else None,
                "fp_contract": args.fp,
                "parallelism": (f"one buffer split in time over {world} GPU(s), first detection by MIN all-reduce"
                                if args.workload == "corr" else f"channels sharded over {world} GPU(s)"),

@@ -63,6 +63,13 @@ __device__ __forceinline__ int32_t limit_t16(int32_t v, unsigned shift) {
     return a > 32767 ? 32767 : (a < -32768 ? -32768 : a);
 }
 
+// pack16(limit_t16(re, shift), limit_t16(im, shift)) in 3 VALU ops: the
+// saturating v_cvt_pk_i16_i32 clamps to exactly [-32768, 32767]
+__device__ __forceinline__ uint32_t limit_t16_pair(int32_t re, int32_t im, unsigned shift) {
+    typedef short s2_t __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, (s2_t)__builtin_amdgcn_cvt_pk_i16(re >> (shift & 31u), im >> (shift & 31u)));
+}
+
 __device__ __forceinline__ int32_t sext16(uint32_t w) { return (int32_t)(int16_t)(w & 0xffffu); }
 __device__ __forceinline__ int32_t sext16_hi(uint32_t w) { return ((int32_t)w) >> 16; }
 __device__ __forceinline__ uint32_t pack16(int32_t re, int32_t im) {

@@ -96,30 +96,45 @@ int launch_ci16(DecimLaunch L, int channels, bool mixed, hipStream_t s) {
 }
 
 // dot2 ci16 kernel shape: tile lanes and mixer table form.  The product ships
-// one shape (512 lanes, doubled mixer table: measured best, profiles/); a
+// one shape (512 lanes, sequence mixer table: measured best, profiles/); a
 // tuning build (-DSRCDSP_TUNING, scripts/tune) can pick another with
 // SRCDSP_CI16_VARIANT = 0: 256 lanes, 1: 512 lanes, 2: 256 lanes + doubled
-// table, 3: 512 lanes + doubled table.
+// table, 3: 512 lanes + doubled table, 4 (product): 512 lanes + sequence table.
 static int ci16_variant() {
 #ifdef SRCDSP_TUNING
     static const int v = [] {
         const char *e = std::getenv("SRCDSP_CI16_VARIANT");
-        return e ? std::atoi(e) : 3;
+        return e ? std::atoi(e) : 4;
     }();
     return v;
 #else
-    return 3;
+    return 4;
 #endif
 }
 
-template <int NT, int BLOCK, bool TAB2>
+// period of the fused mixer's table index over input samples, extended to a
+// multiple of 4 (one 16-B table read per staged granule): lcm(N / gcd(freq, N), 4)
+static unsigned mixer_seq_period(unsigned N, unsigned fr) {
+    unsigned a = N, b = fr;
+    while (b) { const unsigned r = a % b; a = b; b = r; }
+    const unsigned P = N / a;
+    return P % 4 == 0 ? P : (P % 2 == 0 ? 2 * P : 4 * P);
+}
+constexpr unsigned kSeqMax = 4096;  // 2 x 4096 words of LDS, as the doubled phase table
+
+template <int NT, int BLOCK, int TABM>
 int launch_ci16_dot2_shape(DecimLaunch L, int channels, bool mixed, hipStream_t s) {
     constexpr int TO = BLOCK * kCiR;
     L.ntiles = (L.n_out + TO - 1) / TO;
     if (mixed) L.mix_dtile = phase_step_tile(L.mix_N, L.mix_freq, TO);
+    if (mixed && TABM == 2) {
+        L.mix_pe = mixer_seq_period(L.mix_N, L.mix_freq);
+        L.mix_pe_dtile = (unsigned)((4ul * TO) % L.mix_pe);
+        L.mix_pe_drow = (unsigned)((4ul * BLOCK) % L.mix_pe);
+    }
     dim3 grid((unsigned)std::min<long>(L.ntiles, kCfGridCap * 256 / BLOCK), channels);
     if (mixed)
-        hipLaunchKernelGGL((decim_dot2_ci16<NT, BLOCK, true, 4, TAB2>), grid, dim3(BLOCK), 0, s, L);
+        hipLaunchKernelGGL((decim_dot2_ci16<NT, BLOCK, true, 4, TABM>), grid, dim3(BLOCK), 0, s, L);
     else
         hipLaunchKernelGGL((decim_dot2_ci16<NT, BLOCK, false, 4>), grid, dim3(BLOCK), 0, s, L);
     return SRCDSP_OK;
@@ -128,10 +143,16 @@ int launch_ci16_dot2_shape(DecimLaunch L, int channels, bool mixed, hipStream_t 
 template <int NT>
 int launch_ci16_dot2(DecimLaunch L, int channels, bool mixed, hipStream_t s) {
     switch (ci16_variant()) {
-    case 0: return launch_ci16_dot2_shape<NT, 256, false>(L, channels, mixed, s);
-    case 1: return launch_ci16_dot2_shape<NT, 512, false>(L, channels, mixed, s);
-    case 2: return launch_ci16_dot2_shape<NT, 256, true>(L, channels, mixed, s);
-    default: return launch_ci16_dot2_shape<NT, 512, true>(L, channels, mixed, s);
+    case 0: return launch_ci16_dot2_shape<NT, 256, 0>(L, channels, mixed, s);
+    case 1: return launch_ci16_dot2_shape<NT, 512, 0>(L, channels, mixed, s);
+    case 2: return launch_ci16_dot2_shape<NT, 256, 1>(L, channels, mixed, s);
+    case 3: return launch_ci16_dot2_shape<NT, 512, 1>(L, channels, mixed, s);
+    default:
+        // the sequence table (conflict-free reads for any frequency) when its
+        // period fits the LDS budget, else the doubled phase table
+        if (mixed && mixer_seq_period(L.mix_N, L.mix_freq) > kSeqMax)
+            return launch_ci16_dot2_shape<NT, 512, 1>(L, channels, mixed, s);
+        return launch_ci16_dot2_shape<NT, 512, 2>(L, channels, mixed, s);
     }
 }
 

@@ -685,9 +685,17 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream_ci16(DecimLaunch a) 
 // reference's complex<int32_t> arithmetic (host checks |c| <= 32767).
 // Fused mixer (MIX): the LDS table holds (lo T[(k+N/4)%N], hi T[k]) = (lr, li);
 // re = dot2(x, (lr, -li)), im = dot2(swap(x), (lr, li)).
-// LDS: per plane granule G (8 samples), slot 5*(G>>1) + (G&1) + 2*plane, slot
-// 4 of each 5 is padding: the lanes of a ds_read_b128 group (granules 2t+c)
-// land on 16 distinct 16-B bank slots.
+// LDS: plane granule G (8 samples) of plane pl sits in 16-B slot
+//   4p + ((2 pl + (G & 1)) ^ s(p)),  p = G >> 1,  s(p) = ((p>>2)&3) ^ 2((p>>1)&1):
+// no padding; the XOR spreads both access patterns over all 16 bank slots:
+// a ds_read_b128 group's lanes (granules 2t + c) and a ds_write2_b64 group's
+// 16 consecutive lanes (staged granules g -> 8-B halves) are conflict-free
+// (checked exhaustively; the padded 5-slot layout it replaces cost 2-way
+// write conflicts, SQ_LDS_BANK_CONFLICT 30.5 M per 2^28-sample launch).
+__device__ __forceinline__ int dot2_slot(int G, int pl) {
+    const int p = G >> 1;
+    return 4 * p + ((2 * pl + (G & 1)) ^ (((p >> 2) & 3) ^ (2 * ((p >> 1) & 1))));
+}
 __device__ __forceinline__ int32_t clamp_s14(int32_t v) {
     const int32_t a = v >> 14;  // |v| < 2^30: never INT_MIN
     return a > 32767 ? 32767 : (a < -32767 ? -32767 : a);
@@ -707,6 +715,13 @@ __device__ __forceinline__ int32_t sdot2_0(uint32_t a, uint32_t b) {
     int32_t r;
     asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b));
     return r;
+}
+// limitScale16 of a complex<int32_t> accumulator pair for a shift in 1..31
+// (never INT_MIN after the shift): saturating pack, then -32768 -> -32767
+__device__ __forceinline__ uint32_t limit16_pair_sh(int32_t re, int32_t im, unsigned shift) {
+    const short2_t_ p = __builtin_amdgcn_cvt_pk_i16(re >> (shift & 31u), im >> (shift & 31u));
+    const short2_t_ lo = {-32767, -32767};
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(p, lo));
 }
 // two mixer outputs (int32, >> 14 pending) -> one packed int16 pair clamped to
 // +-32767 (limitScale16; |v >> 14| < 2^17 so INT_MIN never occurs):
@@ -906,12 +921,20 @@ __global__ __launch_bounds__(kDtBlock) void decim_tile(DecimLaunch a) {
     }
 }
 
-// TAB2 (mixer): the (lr, li) table stored twice (2N words), so the address of
-// sample j of staged granule i is one add of a wave-uniform tile/granule
-// phase (SGPR) and a per-lane constant (4t + j)*freq mod N -- no per-sample
-// modulo; products via VOP3 dot2 and the pair clamp above.
-template <int NT, int BLOCK, bool MIX, int MINW, bool TAB2 = false>
+// Mixer table forms (TABM):
+//  0: the (lr, li) word of phase k at k (N words);
+//  1 (TAB2): that table stored twice (2N words), so the address of sample j of
+//    staged granule i is one add of a wave-uniform tile/granule phase (SGPR)
+//    and a per-lane constant (4t + j)*freq mod N -- no per-sample modulo.  The
+//    lanes' words sit 4*freq apart: bank conflicts unless freq is odd*16;
+//  2 (sequence table): the word of input SAMPLE s at s mod Pe (Pe = lcm(N /
+//    gcd(freq, N), 4); sample s's phase (phi0 + s*freq) mod N depends on s mod
+//    Pe only), stored twice (2 Pe words).  A lane's 4 samples are 4
+//    consecutive words: one conflict-free ds_read_b128 per granule, any freq.
+// Products via VOP3 dot2 and the pair clamp above.
+template <int NT, int BLOCK, bool MIX, int MINW, int TABM = 0>
 __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
+    constexpr bool TAB2 = TABM == 1, SEQT = TABM == 2;
     constexpr int R = 4;
     constexpr int J = NT / 2 + 1;                 // tap pairs
     constexpr int HS = 16 * ceildiv(2 * (J - 1), 16);  // halo samples (lane-chunk aligned)
@@ -920,11 +943,11 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     constexpr int TG = (4 * TO + HS) / 4;         // staged 16-B sample granules
     constexpr int PER = ceildiv(TG, BLOCK);
     constexpr int PG = (4 * TO + HS) / 8;         // plane granules
-    constexpr int LSLOTS = 5 * ceildiv(PG, 2);
-    constexpr int TABMAX = MIX ? (TAB2 ? 8192 : 4096) : 1;
+    constexpr int LSLOTS = 4 * ceildiv(PG, 2);
+    constexpr int TABMAX = MIX ? (TABM ? 8192 : 4096) : 1;
     static_assert(HS % 16 == 0 && 2 * (J - 1) <= HS, "halo geometry");
     __shared__ uint4 lds[LSLOTS];
-    __shared__ uint32_t ctab[TABMAX];
+    __shared__ __attribute__((aligned(16))) uint32_t ctab[TABMAX];
 
     const int ch = blockIdx.y;
     const uint32_t *in = (const uint32_t *)a.in + ch * a.in_stride;
@@ -940,10 +963,18 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     const long t_begin = b * per + (b < rem ? b : rem);
     const long t_end = t_begin + per + (b < rem ? 1 : 0);
 
+    const unsigned Pe = SEQT ? a.mix_pe : 1u;
     if constexpr (MIX) {
         const int16_t *tab = a.mix_table;
-        for (int i = t; i < (TAB2 ? 2 : 1) * (int)N; i += BLOCK) {
-            const unsigned k = (unsigned)i < N ? (unsigned)i : (unsigned)i - N;
+        const int nw = SEQT ? 2 * (int)Pe : (TAB2 ? 2 : 1) * (int)N;
+        for (int i = t; i < nw; i += BLOCK) {
+            unsigned k;
+            if constexpr (SEQT) {
+                const unsigned m = (unsigned)i < Pe ? (unsigned)i : (unsigned)i - Pe;
+                k = (unsigned)(((unsigned long)a.mix_phase0 + (unsigned long)m * fr) % N);
+            } else {
+                k = (unsigned)i < N ? (unsigned)i : (unsigned)i - N;
+            }
             unsigned ic = k + N / 4;
             ic = ic >= N ? ic - N : ic;
             ctab[i] = ((uint32_t)(uint16_t)tab[ic]) | ((uint32_t)(uint16_t)tab[k] << 16);
@@ -957,14 +988,18 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
         mix_dot2(w, ctab[ph], re, im);
         return pack16(re, im);
     };
+    // input sample s >= 0 of this call, mixed (any table form)
+    auto mix_at = [&](uint32_t w, long s) {
+        if constexpr (SEQT) return mix1(w, (unsigned)(s % (long)Pe));
+        else return mix1(w, phase_add(a.mix_phase0, (unsigned)(s % (long)N)));
+    };
     if (t_begin == 0 && t_end > 0) {  // new history = last H samples of (history ++ mixed input)
         uint32_t *ho = (uint32_t *)a.hist_out[ch];
         for (int k = t; k < H; k += BLOCK) {
             long idx = n_in - H + k;
             uint32_t w = idx >= 0 ? in[idx] : hist[H + idx];
             if constexpr (MIX)
-                if (idx >= 0) w = mix1(w, idx < k ? phase_add(a.mix_phase0, (unsigned)idx)
-                                                  : phase_add(a.mix_phase_hist, (unsigned)k));
+                if (idx >= 0) w = mix_at(w, idx);
             ho[k] = w;
         }
     }
@@ -992,7 +1027,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     // staged granule g -> plane granule g>>1, half g&1
     auto lds_half = [&](int g, int plane) {
         const int G = g >> 1;
-        return (uint2 *)&lds[5 * (G >> 1) + (G & 1) + 2 * plane] + (g & 1);
+        return (uint2 *)&lds[dot2_slot(G, plane)] + (g & 1);
     };
     auto put = [&](int g, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
         *lds_half(g, 0) = make_uint2(lo16_pair(w0, w1), lo16_pair(w2, w3));
@@ -1019,6 +1054,29 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
         *lds_half(g, 0) = make_uint2(clamp_pair_s14(r0, r1), clamp_pair_s14(r2, r3));
         *lds_half(g, 1) = make_uint2(clamp_pair_s14(i0, i1), clamp_pair_s14(i2, i3));
     };
+    // SEQT: the granule's 4 words at ctab[m + lane offset], m = (first staged
+    // sample of the granule row) mod Pe (uniform); lane offset 4t mod Pe
+    const unsigned lo_t = SEQT ? (4u * t) % Pe : 0u;
+    auto put_mixed_seq = [&](int g, uint4 w, unsigned m) {
+        // m + lo_t is a multiple of 4 words: one 16-B read (the compiler, not
+        // knowing that, would split it into 4-way-conflicting ds_read2_b32)
+        const uint4 c = *(const uint4 *)__builtin_assume_aligned(&ctab[m + lo_t], 16);
+        auto neg_hi = [](uint32_t x) {
+            return __builtin_bit_cast(uint32_t, __builtin_bit_cast(short2_t_, x) * (short2_t_){1, -1});
+        };
+        auto swp = [](uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); };
+        const int32_t r0 = sdot2_0(w.x, neg_hi(c.x)), i0 = sdot2_0(swp(w.x), c.x);
+        const int32_t r1 = sdot2_0(w.y, neg_hi(c.y)), i1 = sdot2_0(swp(w.y), c.y);
+        const int32_t r2 = sdot2_0(w.z, neg_hi(c.z)), i2 = sdot2_0(swp(w.z), c.z);
+        const int32_t r3 = sdot2_0(w.w, neg_hi(c.w)), i3 = sdot2_0(swp(w.w), c.w);
+        *lds_half(g, 0) = make_uint2(clamp_pair_s14(r0, r1), clamp_pair_s14(r2, r3));
+        *lds_half(g, 1) = make_uint2(clamp_pair_s14(i0, i1), clamp_pair_s14(i2, i3));
+    };
+    auto advp = [&](unsigned p, unsigned d) { p += d; const unsigned q = p - Pe; return q < p ? q : p; };
+    // SEQT: (4*tile*TO - HS) mod Pe of the workgroup's current tile
+    unsigned m_tile = 0;
+    if constexpr (MIX && SEQT)
+        if (t_begin < t_end) m_tile = (unsigned)((4 * t_begin * (long)TO - HS + 4 * (long)Pe * (1 + HS / 4)) % (long)Pe);
     auto put_mixed = [&](int g, uint4 w, unsigned ph) {
         if constexpr (MIX) {
             int32_t r0, i0, r1, i1, r2, i2, r3, i3;
@@ -1045,7 +1103,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
                     for (int j = 0; j < 4; ++j) {
                         w[j] = fetch(in, hist, s0 + j, n_in, H);
                         if constexpr (MIX)
-                            if (s0 + j >= 0 && s0 + j < n_in) w[j] = mix1(w[j], phase_add(a.mix_phase0, (unsigned)(s0 + j)));
+                            if (s0 + j >= 0 && s0 + j < n_in) w[j] = mix_at(w[j], s0 + j);
                     }
                     v[i] = make_uint4(w[0], w[1], w[2], w[3]);
                 }
@@ -1057,7 +1115,15 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     const int lb = 2 * t + HG;  // lane's first plane granule
     for (long tile = t_begin; tile < t_end; ++tile) {
         SRCDSP_LDS_BARRIER();
-        if (MIX && TAB2 && tile != 0) {
+        if (MIX && SEQT && tile != 0) {
+            unsigned m = m_tile;  // wave-uniform
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int g = t + i * BLOCK;
+                if (g < TG) put_mixed_seq(g, v[i], m);
+                m = advp(m, a.mix_pe_drow);
+            }
+        } else if (MIX && TAB2 && tile != 0) {
             unsigned sp = tile_phase(tile);  // wave-uniform
 #pragma unroll
             for (int i = 0; i < PER; ++i) {
@@ -1081,6 +1147,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
             }
         }
         SRCDSP_LDS_BARRIER();
+        if constexpr (MIX && SEQT) m_tile = advp(m_tile, a.mix_pe_dtile);
         if (tile + 1 < t_end) stage_load(tile + 1);
 
         ConstPtr<uint32_t> tp = const_view<uint32_t>(a.coef);
@@ -1090,10 +1157,15 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
         constexpr int OFF = 4 * NG;
         uint32_t Dr[OFF + 8], Di[OFF + 8];
         auto load_g = [&](int c) {  // plane granule lb + c -> dwords d = 4c .. 4c+3
-            const uint4 gr = lds[5 * ((lb + c) >> 1) + ((lb + c) & 1)];
-            const uint4 gi = lds[5 * ((lb + c) >> 1) + ((lb + c) & 1) + 2];
-            Dr[OFF + 4 * c + 0] = gr.x; Dr[OFF + 4 * c + 1] = gr.y; Dr[OFF + 4 * c + 2] = gr.z; Dr[OFF + 4 * c + 3] = gr.w;
-            Di[OFF + 4 * c + 0] = gi.x; Di[OFF + 4 * c + 1] = gi.y; Di[OFF + 4 * c + 2] = gi.z; Di[OFF + 4 * c + 3] = gi.w;
+            typedef uint32_t u4v_t __attribute__((ext_vector_type(4)));
+            u4v_t gr = *(const u4v_t *)&lds[dot2_slot(lb + c, 0)];
+            u4v_t gi = *(const u4v_t *)&lds[dot2_slot(lb + c, 1)];
+            // keep every read a whole ds_read_b128: at the window edges the
+            // compiler would load only the words used, as ds_read2_b32 /
+            // ds_read_b96, whose 4-B lane groups the layout does not spread
+            asm volatile("" : "+v"(gr), "+v"(gi));
+            Dr[OFF + 4 * c + 0] = gr[0]; Dr[OFF + 4 * c + 1] = gr[1]; Dr[OFF + 4 * c + 2] = gr[2]; Dr[OFF + 4 * c + 3] = gr[3];
+            Di[OFF + 4 * c + 0] = gi[0]; Di[OFF + 4 * c + 1] = gi[1]; Di[OFF + 4 * c + 2] = gi[2]; Di[OFF + 4 * c + 3] = gi[3];
         };
         load_g(0);
         load_g(1);
@@ -1113,7 +1185,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
         }
         const long n0 = tile * TO + (long)t * R;
         const unsigned sh = a.shift;
-        if (n0 + R <= a.n_out) {
+        if (n0 + R <= a.n_out && (sh & 31u) != 0) {  // Q14 taps: shift 14 (the common case)
+            *(uint4 *)(out + n0) = make_uint4(limit16_pair_sh(yr[0], yi[0], sh), limit16_pair_sh(yr[1], yi[1], sh),
+                                              limit16_pair_sh(yr[2], yi[2], sh), limit16_pair_sh(yr[3], yi[3], sh));
+        } else if (n0 + R <= a.n_out) {
             *(uint4 *)(out + n0) = make_uint4(pack16(limit16(yr[0], sh), limit16(yi[0], sh)),
                                               pack16(limit16(yr[1], sh), limit16(yi[1], sh)),
                                               pack16(limit16(yr[2], sh), limit16(yi[2], sh)),

@@ -62,6 +62,10 @@ struct DecimLaunch {
     unsigned mix_phase_tile0;  // phase of tile 0's first staged sample (index -4*NQ)
     unsigned mix_dtile;        // phase advance per tile (4*TO samples)
     unsigned mix_phase_hist;   // phase of input sample n_in - H (history write-back)
+    // sequence-table mixer (decim_dot2_ci16 TABM = 2): the table holds the
+    // (cos, sin) word of input sample s at s mod mix_pe, mix_pe = lcm(period of
+    // s*freq mod N, 4); per-tile / per-granule-row advances of that index
+    unsigned mix_pe, mix_pe_dtile, mix_pe_drow;
     const void *hist_in[kMaxBatch];
     void *hist_out[kMaxBatch];
 };

@@ -86,7 +86,7 @@ __global__ __launch_bounds__(256) void up_kernel(const void *in, long n_in, long
             for (int i = 0; i < H; ++i) up_mac<UV>(yr, yi, c[i], up_fetch<UV>(in, hist_in, j - i, n_in, Hm1));
             const long oi = (long)L * j + o;
             if (UV == UV_I16_I32) ((int16_t *)out)[oi] = (int16_t)limit_t16((int32_t)yr, shift);
-            else ((uint32_t *)out)[oi] = pack16(limit_t16((int32_t)yr, shift), limit_t16((int32_t)yi, shift));
+            else ((uint32_t *)out)[oi] = limit_t16_pair((int32_t)yr, (int32_t)yi, shift);
         }
     }
 }
@@ -198,7 +198,7 @@ __global__ __launch_bounds__(kUpBlock) void up_tile(const uint32_t *in, long n_i
         if (j >= n_total) break;
         uint32_t w[LR];
 #pragma unroll
-        for (int o = 0; o < LR; ++o) w[o] = pack16(limit_t16((int32_t)yr[o][r], shift), limit_t16((int32_t)yi[o][r], shift));
+        for (int o = 0; o < LR; ++o) w[o] = limit_t16_pair((int32_t)yr[o][r], (int32_t)yi[o][r], shift);
         uint32_t *dst = out + (long)LR * j;
 #pragma unroll
         for (int o = 0; o < LR; o += 2) *(uint2 *)(dst + o) = make_uint2(w[o], w[o + 1]);
@@ -341,7 +341,7 @@ __global__ __launch_bounds__(kUpBlockD) void up_tile_dot2(const uint32_t *in, lo
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int idx = 4 * k + u, r = idx / LR, o = idx % LR;
-            w4[u] = pack16(limit_t16(yr[o][r], shift), limit_t16(yi[o][r], shift));
+            w4[u] = limit_t16_pair(yr[o][r], yi[o][r], shift);
         }
         ob[t * STR + k] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
     }

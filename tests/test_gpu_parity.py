@@ -200,10 +200,14 @@ def test_decim_ci16_tap_ranges_vs_oracle(S, O, ntaps, kind):
         assert np.array_equal(g.step(dev(xs)).cpu().numpy(), r.step(xs)), (off, n)
 
 
-@pytest.mark.parametrize("N,f", [(1000, -0.37), (4096, 0.73), (2048, 0.0)])
+@pytest.mark.parametrize("N,f", [(1000, -0.37), (4096, 0.73), (2048, 0.0), (4096, 0.1), (4096, 0.5),
+                                 (3000, 0.3), (1022, 0.9), (4093, 0.1), (4096, -1.0 / 1024)])
 def test_mixdecim_chain_table_sizes(S, O, N, f):
     """Fused mixer (LDS (cos, sin) table, dot2 complex multiply) at
-    non-power-of-two and power-of-two table sizes, several chained calls."""
+    non-power-of-two and power-of-two table sizes, several chained calls.
+    The sequence table's period Pe = lcm(N / gcd(freq, N), 4) spans 4 (f = 0,
+    0.5), 20, 200, 2044 (lane offsets wrap), 4096, and 16372 for N = 4093
+    (over the LDS budget: the doubled phase table instead)."""
     from srcdsp_amd.design import hamming_sinc, q14
     cq = q14(hamming_sinc(127))
     x = O["strict"].gen_ci16(0xBEE, 3, 0, 400000, -32768, 32767)
