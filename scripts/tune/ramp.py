@@ -53,7 +53,15 @@ def main():
     t0buf = torch.zeros(1, dtype=torch.int64, device="cuda")
     torch.cuda.synchronize()
 
-    def launch():
+    # VARIANT may be a sequence "A*n,B*m,...": n launches of A, then m of B
+    # (e.g. "70*8,71*40": the memory path timed at the clock the product left)
+    seq = []
+    for part in var.split(","):
+        v, _, k = part.partition("*")
+        seq += [v] * (int(k) if k else n)
+    n = len(seq)
+
+    def launch(var):
         if var == "prod":
             f.step(x, y)
         elif var == "read":
@@ -72,7 +80,7 @@ def main():
     lib.tune_realtime_stamp(C.c_void_p(t0buf.data_ptr()), st)
     for i in range(n):
         ev[i][0].record(main_s)
-        launch()
+        launch(seq[i])
         ev[i][1].record(main_s)
     torch.cuda.synchronize()
     ms = np.array([a.elapsed_time(b) for a, b in ev])
@@ -88,7 +96,7 @@ def main():
         sel = (mid >= a) & (mid < a + d)
         ghz.append(float(np.mean(clk[sel])) if sel.any() else float("nan"))
     idle = clk[mid < -1.0]
-    out = {"variant": var, "launches": n, "idle_ghz": round(float(np.median(idle)), 3) if idle.size else None,
+    out = {"variant": var, "launches": n, "seq": seq, "idle_ghz": round(float(np.median(idle)), 3) if idle.size else None,
            "ms": [round(float(v), 4) for v in ms], "ghz": [round(v, 3) for v in ghz],
            "ms_6_25": round(float(np.mean(ms[5:25])), 4), "ms_last100": round(float(np.mean(ms[-100:])), 4),
            "ghz_6_25": round(float(np.nanmean(ghz[5:25])), 3), "ghz_last100": round(float(np.nanmean(ghz[-100:])), 3)}

@@ -180,6 +180,21 @@ extern "C" int tune_decim(int variant, int grid, const float *d_coef, const void
     case 94: L.ntiles = tiles(384 * 4); return launch(decim_stream2_cf32<127, 4, 384, true, 3, true, 1, true, 2, true, true>, grid, 384, L, s);
     case 95: L.ntiles = tiles(768 * 4); return launch(decim_stream2_cf32<127, 4, 768, true, 3, true, 1, true, 2, true, true>, grid, 768, L, s);
     case 96: L.ntiles = tiles(384 * 4); return launch(decim_stream2_cf32<127, 4, 384, true, 4, true, 0, true, 2, true, true>, grid, 384, L, s);
+    case 76: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 4, true, 2, true, true>, grid, 512, L, s);
+    case 77: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 5, true, 2, true, true>, grid, 512, L, s);
+    case 205: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 4, true, 2, true, true, -1, -1, true>, grid, 512, L, s);
+    case 206: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 5, true, 2, true, true, -1, -1, true>, grid, 512, L, s);
+    // wave-private images, no barriers (decim_wave_cf32): 256-output wave tiles
+    case 400: L.ntiles = tiles(256); return launch(decim_wave_cf32<127, 512, true, 4, true>, grid, 512, L, s);
+    case 401: L.ntiles = tiles(256); return launch(decim_wave_cf32<127, 256, true, 4, true>, grid, 256, L, s);
+    case 402: L.ntiles = tiles(256); return launch(decim_wave_cf32<127, 512, true, 4, true, 1>, grid, 512, L, s);
+    case 403: L.ntiles = tiles(256); return launch(decim_wave_cf32<127, 512, true, 4, true, 2>, grid, 512, L, s);
+    case 404: L.ntiles = tiles(256); return launch(decim_wave_cf32<127, 512, true, 4, true, 1, 0>, grid, 512, L, s);
+    case 405: L.ntiles = tiles(256); return launch(decim_wave_cf32<127, 512, true, 4, true, 3>, grid, 512, L, s);
+    case 406: L.ntiles = tiles(256); return launch(decim_wave_cf32<127, 512, true, 4, true, 0, 0>, grid, 512, L, s);
+    case 407: L.ntiles = tiles(256); return launch(decim_wave_cf32<127, 256, true, 4, true, 1>, grid, 256, L, s);
+    case 408: L.ntiles = tiles(256); return launch(decim_wave_cf32<127, 512, true, 4, true, 1, 2, true>, grid, 512, L, s);
+    case 409: L.ntiles = tiles(256); return launch(decim_wave_cf32<127, 512, true, 4, true, 0, 2, true>, grid, 512, L, s);
     case 75: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, 0, true, true>, grid, 512, L, s);
     case 24: L.ntiles = tiles(128 * 8); return launch(decim_stream2_cf32<127, 8, 128, true, 2, true>, grid, 128, L, s);
     default: return -1;

@@ -67,9 +67,12 @@ int launch_cf32(DecimLaunch L, int channels, bool fma, hipStream_t s) {
     // (8192 samples: half the halo re-read of 256), grid-stride tile order,
     // non-temporal input loads, outputs paired across half-waves by
     // v_permlane32_swap into whole-line non-temporal stores (no LDS round
-    // trip: 2 barriers per tile, not 4); 2 workgroups (16 waves) per CU
+    // trip: 2 barriers per tile, not 4); 2 workgroups (16 waves) per CU;
+    // taps issued tap-major through inline asm (ILV; FMA: 0.88 M instead of
+    // 1.08 M cycles per launch, -8.6 % time on one box,
+    // profiles/tuning/r02_ramp_ab.txt)
 #define SRCDSP_CF32(F, Q) \
-    hipLaunchKernelGGL((decim_stream2_cf32<NT, kCfR, kCfBlock, F, 4, Q, 0, true, 2, true, true>), grid, \
+    hipLaunchKernelGGL((decim_stream2_cf32<NT, kCfR, kCfBlock, F, 4, Q, 0, true, 2, true, true, -1, -1, true>), grid, \
                        dim3(kCfBlock), 0, s, L)
     if (fma && q0)
         SRCDSP_CF32(true, true);

@@ -28,6 +28,21 @@ __device__ __forceinline__ void pk_fma_tap(f2_t &acc, unsigned long long cp, f2_
         asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[0,1,1]" : "+v"(acc) : "s"(cp), "v"(x));
 }
 
+// The strict contract's step acc = acc + c*x (separately rounded product,
+// then sum, as the reference's -O2 x86-64 build computes it), split so a
+// tap's R products can issue before its R sums: pk_mul_tap writes the
+// product, pk_add_acc adds it.
+template <bool HI>
+__device__ __forceinline__ void pk_mul_tap(f2_t &p, unsigned long long cp, f2_t x) {
+    if constexpr (HI)
+        asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(p) : "s"(cp), "v"(x));
+    else
+        asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(p) : "s"(cp), "v"(x));
+}
+__device__ __forceinline__ void pk_add_acc(f2_t &acc, f2_t p) {
+    asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(acc) : "v"(p));
+}
+
 // ------------------------------------------------------------ arithmetic
 template <bool FMA>
 __device__ __forceinline__ float mac(float c, float x, float y) {
@@ -188,7 +203,9 @@ __device__ __forceinline__ float q16f_shift0(float y) {
 //    so the tail needs no per-lane compare) -- fewer VALU ops per load;
 //  * Q0: the shift-0 quantiser above (host selects it when shift & 31 == 0).
 // PROBE (tuning only): 0 = real kernel; 1 = memory path only (no FMA loop);
-// 2 = compute path only (every tile reads the same L2-resident input span)
+// 2 = compute path only (every tile reads the same L2-resident input span);
+// 4 = no staging after the first tile (the tap loop over one LDS image, with
+// the stores); 5 = as 4 without the stores
 // NTL: non-temporal (streaming) input loads; OST: outputs staged through LDS
 // so each store instruction writes whole contiguous lines; NTS: non-temporal
 // output stores; GS: grid-stride tile order (else a contiguous run of tiles
@@ -262,7 +279,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
     static_assert(OST != 2 || R == 4 || R == 8, "whole-line stores assume 4 or 8 outputs per lane");
 #ifndef SRCDSP_TUNING
     // the probe / cache-policy / issue-order variants exist for scripts/tune only
-    static_assert(PROBE == 0 && LAUX < 0 && SAUX < 0 && !ILV, "tuning-only variant: build with -DSRCDSP_TUNING");
+    static_assert(PROBE == 0 && LAUX < 0 && SAUX < 0, "tuning-only variant: build with -DSRCDSP_TUNING");
 #endif
     constexpr int NQ = (NT + 3) / 4;
     constexpr int TO = BLOCK * R;
@@ -364,15 +381,20 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
         };
 #pragma unroll
         for (int e = -1; e < R; ++e) load_group(e);
-        if constexpr (PROBE == 1) {
+        if constexpr (PROBE == 1 || PROBE == 3) {
 #pragma unroll
             for (int r = 0; r < R; ++r) { yr[r] = X[4 * r + 4 * NQ].x; yi[r] = X[4 * r + 4 * NQ].y; }
-        } else if constexpr (ILV && FMA && PROBE != 3) {
-            // tap-major issue order through pk_fma_tap: R independent chains
-            // round-robin, taps as SGPR pairs (c[2m], c[2m+1])
+        } else if constexpr (ILV && PROBE != 3) {
+            // tap-major issue order through inline asm: R independent chains
+            // round-robin, taps as SGPR pairs (c[2m], c[2m+1]); FMA: one
+            // pk_fma per tap and output; strict: R products, then R sums
             ConstPtr<unsigned long long> tp2 = const_view<unsigned long long>(a.coef);
             asm volatile("" : "+s"(tp2));
             f2_t acc[R];
+            if constexpr (!FMA) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) acc[r] = f2_t{0.f, 0.f};
+            }
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 if (q + 1 < NQ) load_group(-q - 2);
@@ -382,13 +404,26 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
                     const int k = 4 * q + p;
                     if (k < NT) {
                         const unsigned long long cp = tp2[k >> 1];
+                        if constexpr (FMA) {
 #pragma unroll
-                        for (int r = 0; r < R; ++r) {
-                            const float2 x = X[4 * (r - q) - p + 4 * NQ];
-                            const f2_t xv = {x.x, x.y};
-                            if (k == 0) pk_fma_tap<false, true>(acc[r], cp, xv);
-                            else if (k & 1) pk_fma_tap<true, false>(acc[r], cp, xv);
-                            else pk_fma_tap<false, false>(acc[r], cp, xv);
+                            for (int r = 0; r < R; ++r) {
+                                const float2 x = X[4 * (r - q) - p + 4 * NQ];
+                                const f2_t xv = {x.x, x.y};
+                                if (k == 0) pk_fma_tap<false, true>(acc[r], cp, xv);
+                                else if (k & 1) pk_fma_tap<true, false>(acc[r], cp, xv);
+                                else pk_fma_tap<false, false>(acc[r], cp, xv);
+                            }
+                        } else {
+                            f2_t pr[R];
+#pragma unroll
+                            for (int r = 0; r < R; ++r) {
+                                const float2 x = X[4 * (r - q) - p + 4 * NQ];
+                                const f2_t xv = {x.x, x.y};
+                                if (k & 1) pk_mul_tap<true>(pr[r], cp, xv);
+                                else pk_mul_tap<false>(pr[r], cp, xv);
+                            }
+#pragma unroll
+                            for (int r = 0; r < R; ++r) pk_add_acc(acc[r], pr[r]);
                         }
                     }
                 }
@@ -418,7 +453,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
         const long n0 = tile * TO + (long)t * R;
         const unsigned sh = a.shift;
         auto q = [&](float y) { return Q0 ? q16f_shift0(y) : q16f(y, sh); };
-        if constexpr (OST == 2 && WHOLE) {
+        if (PROBE == 5 && a.ntaps != 12345) {  // tuning: no stores
+        } else if constexpr (OST == 2 && WHOLE) {
             float2 o[R];
 #pragma unroll
             for (int r = 0; r < R; ++r) o[r] = make_float2(q(yr[r]), q(yi[r]));
@@ -476,9 +512,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
         stage_to_lds();
         long tile = t_begin;
         for (; tile + t_step < t_end; tile += t_step) {
-            stage_load(v, tile + t_step);
+            if constexpr (PROBE < 4) stage_load(v, tile + t_step);
             do_tile(tile, std::true_type{});
-            stage_to_lds();
+            if constexpr (PROBE < 4) stage_to_lds();
         }
         if ((tile + 1) * TO <= a.n_out)
             do_tile(tile, std::true_type{});
@@ -1500,6 +1536,204 @@ __global__ __launch_bounds__(kFirBlock, 4) void fir_stream_f32(DecimLaunch a) {
         else
             do_tile(tile, std::false_type{});
     }
+}
+
+}  // namespace srcdsp
+namespace srcdsp {
+
+// ------------------------------------------------- wave-private cf32 (headline)
+// Persistent complex<float> decimator, M = 4, with NO workgroup barrier: every
+// wave owns wave tiles of 64 lanes x 4 outputs (1024 input samples + the
+// 4*NQ-sample halo) end to end -- loads, LDS image, taps, stores.
+//
+// The wave's LDS image is stored column-major: image granule g (16 B, two
+// samples) = column g/8, row g%8 sits at slot row*NCOL + column.  Column c is
+// lane (c - HC)'s 8-granule chunk (HC halo columns first).  So
+//  * lane t's read of its frame group e (granules 2e, 2e+1 of its chunk) is
+//    slot ((2e)&7)*NCOL + HC + t + floor(2e/8): a per-lane base (16 t) plus a
+//    compile-time immediate, and the 16 lanes of a ds_read_b128 group read 16
+//    consecutive slots -- conflict-free without any pad granules;
+//  * load instruction i, lane l fetches the contiguous image granule 64 i + l
+//    and writes it to slot (l&7)*NCOL + 8i + l/8; with NCOL = 1 (mod 8) the 8
+//    lanes of a ds_write_b128 group land in 8 distinct 16-B bank slots.
+// One image is 8*NCOL*16 B (9,344 B at NQ = 32), so 16 waves fit a CU's LDS
+// with one image each.  A wave lands its prefetched next tile as soon as its
+// own reads of the current image are done (LDS operations of one wave execute
+// in order), so no wave ever waits for another: the four waves of a SIMD
+// drift apart and keep the VALU fed.  The halo (the previous wave tile's
+// tail) is re-read by every wave tile, an L2 hit.
+// Taps: wave-uniform SGPR pairs, issued tap-major (pk_fma_tap) for the FMA
+// contract; the strict contract keeps separately rounded mul/add.
+// PROBE (tuning only): 1 = memory path only (no tap loop); 2 = compute path
+// only (every wave tile loads one of 16 L2-resident spans)
+// 3 = memory path without the halo load; LAUX: load cache policy (2 = nt)
+// SYNC (tuning): one workgroup barrier per wave tile, before its loads issue
+template <int NT, int BLOCK, bool FMA, int MINW, bool Q0, int PROBE = 0, int LAUX = 2, bool SYNC = false>
+__global__ __launch_bounds__(BLOCK, MINW) void decim_wave_cf32(DecimLaunch a) {
+#ifndef SRCDSP_TUNING
+    static_assert(PROBE == 0 && LAUX == 2 && !SYNC, "tuning-only variant: build with -DSRCDSP_TUNING");
+#endif
+    constexpr int R = 4;                      // outputs per lane
+    constexpr int NQ = (NT + 3) / 4;          // 4-tap polyphase groups
+    constexpr int HC = ceildiv(2 * NQ, 8);    // halo columns (8 granules each)
+    constexpr int COLS = 64 + HC;             // loaded columns
+    constexpr int NCOL = COLS + ((1 - COLS % 8) + 8) % 8;  // = 1 (mod 8)
+    constexpr int WG = 8 * COLS;              // image granules (loaded)
+    static_assert(WG % 64 == 0, "whole load instructions per image");
+    constexpr int PER = WG / 64;              // loads per lane
+    constexpr int WPB = BLOCK / 64;
+    constexpr int TO = 64 * R;                // outputs per wave tile
+    constexpr int HALO = 8 * HC * 2;          // halo samples (>= 4 NQ)
+    __shared__ float4 lds[WPB][8 * NCOL];
+
+    const int ch = blockIdx.y;
+    const float2 *in = (const float2 *)a.in + ch * a.in_stride;
+    const float2 *hist = (const float2 *)a.hist_in[ch];
+    float2 *out = (float2 *)a.out + ch * a.out_stride;
+    const long n_in = a.n_in;
+    const int H = NT - 1;
+    const int ln = threadIdx.x & 63;
+    // wave index made wave-uniform for the compiler: tiles, descriptors and
+    // the image base live in SGPRs
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const long nb = gridDim.x;
+    const long b = xcd_tile(blockIdx.x, nb);
+    if (b == 0) write_history(in, n_in, hist, (float2 *)a.hist_out[ch], H);
+    float4 *img = lds[wv];
+    const long step = nb * WPB;
+    long tile = b * WPB + wv;
+
+    float4 v[PER];
+    // image granule 64 i + ln of wave tile `tile` (>= 1): one descriptor per
+    // tile, range-checked (zero past the input end), non-temporal
+    auto stage_load = [&](long tl) {
+        if constexpr (PROBE == 2) tl = 1 + (tl & 15);
+        const long s0 = (long)TO * 4 * tl - HALO;
+        const long remb = (n_in - s0) * 8;
+        const unsigned nrec = (unsigned)(remb > 0xfffffff0L ? 0xfffffff0L : (remb < 0 ? 0 : remb));
+        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)(in + s0), 0, nrec, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            if (PROBE == 3 && i == 0) { v[i] = make_float4(0.f, 0.f, 0.f, 0.f); continue; }
+            auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * ln, 1024 * i, LAUX);
+            v[i] = make_float4(__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]),
+                               __uint_as_float(w[3]));
+        }
+    };
+    auto stage_first = [&]() {  // wave tile 0: the halo comes from the history
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const long s = -HALO + 2 * (long)(64 * i + ln);
+            const float2 lo = fetch(in, hist, s, n_in, H), hi = fetch(in, hist, s + 1, n_in, H);
+            v[i] = make_float4(lo.x, lo.y, hi.x, hi.y);
+        }
+    };
+    const int wslot = (ln & 7) * NCOL + (ln >> 3);
+    auto land = [&]() {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) img[wslot + 8 * i] = v[i];
+    };
+    // own frame of lane ln: granule 2e (+1) -> slot ((2e)&7)*NCOL + HC + ln + floor(2e/8)
+    const float4 *rd = img + HC + ln;
+    auto do_tile = [&](long tl, auto whole_tag) {
+        constexpr bool WHOLE = decltype(whole_tag)::value;
+        float2 X[4 * (NQ + R)];
+        auto load_group = [&](int e) {
+            const int o = ((2 * e) & 7) * NCOL + floordiv(2 * e, 8);
+            const float4 g0 = rd[o], g1 = rd[o + NCOL];
+            X[4 * e + 4 * NQ + 0] = make_float2(g0.x, g0.y);
+            X[4 * e + 4 * NQ + 1] = make_float2(g0.z, g0.w);
+            X[4 * e + 4 * NQ + 2] = make_float2(g1.x, g1.y);
+            X[4 * e + 4 * NQ + 3] = make_float2(g1.z, g1.w);
+        };
+#pragma unroll
+        for (int e = -1; e < R; ++e) load_group(e);
+        float yr[R], yi[R];
+        if constexpr (PROBE == 1 || PROBE == 3) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) { yr[r] = X[4 * r + 4 * NQ].x; yi[r] = X[4 * r + 4 * NQ - 4].y; }
+        } else if constexpr (FMA) {
+            ConstPtr<unsigned long long> tp2 = const_view<unsigned long long>(a.coef);
+            asm volatile("" : "+s"(tp2));
+            f2_t acc[R];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                if (q + 1 < NQ) load_group(-q - 2);
+                if ((q & 3) == 0) asm volatile("" : "+s"(tp2));
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    const int k = 4 * q + p;
+                    if (k < NT) {
+                        const unsigned long long cp = tp2[k >> 1];
+#pragma unroll
+                        for (int r = 0; r < R; ++r) {
+                            const float2 x = X[4 * (r - q) - p + 4 * NQ];
+                            const f2_t xv = {x.x, x.y};
+                            if (k == 0) pk_fma_tap<false, true>(acc[r], cp, xv);
+                            else if (k & 1) pk_fma_tap<true, false>(acc[r], cp, xv);
+                            else pk_fma_tap<false, false>(acc[r], cp, xv);
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r) { yr[r] = acc[r].x; yi[r] = acc[r].y; }
+        } else {
+            ConstPtr<float> tp = const_view<float>(a.coef);
+            asm volatile("" : "+s"(tp));
+#pragma unroll
+            for (int r = 0; r < R; ++r) yr[r] = yi[r] = 0.f;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                if (q + 1 < NQ) load_group(-q - 2);
+                if ((q & 3) == 0) asm volatile("" : "+s"(tp));
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    const int k = 4 * q + p;
+                    if (k < NT) {
+                        const float c = tp[k];
+#pragma unroll
+                        for (int r = 0; r < R; ++r) {
+                            const float2 x = X[4 * (r - q) - p + 4 * NQ];
+                            yr[r] = mac<false>(c, x.x, yr[r]);
+                            yi[r] = mac<false>(c, x.y, yi[r]);
+                        }
+                    }
+                }
+            }
+        }
+        const unsigned sh = a.shift;
+        auto qz = [&](float y) { return Q0 ? q16f_shift0(y) : q16f(y, sh); };
+        const long o0 = tl * TO;
+        if constexpr (WHOLE) {
+            float2 o[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) o[r] = make_float2(qz(yr[r]), qz(yi[r]));
+            store_wave_lines<R, true>(out + o0, o, ln);
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const long n = o0 + (long)ln * R + r;
+                if (n < a.n_out) out[n] = make_float2(qz(yr[r]), qz(yi[r]));
+            }
+        }
+    };
+    if (tile >= a.ntiles) return;
+    if (tile == 0) stage_first(); else stage_load(tile);
+    // land this tile, issue the next one's loads, then the taps and stores:
+    // the wait for the prefetch (next iteration's land) leaves the stores in
+    // flight; the wave's last tile is peeled so the loop body is straight
+    for (; tile + step < a.ntiles; tile += step) {
+        land();
+        if constexpr (SYNC) __builtin_amdgcn_s_barrier();
+        stage_load(tile + step);
+        do_tile(tile, std::true_type{});
+    }
+    land();
+    if ((tile + 1) * TO <= a.n_out)
+        do_tile(tile, std::true_type{});
+    else
+        do_tile(tile, std::false_type{});
 }
 
 }  // namespace srcdsp
