@@ -721,16 +721,19 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream_ci16(DecimLaunch a) 
 // reference's complex<int32_t> arithmetic (host checks |c| <= 32767).
 // Fused mixer (MIX): the LDS table holds (lo T[(k+N/4)%N], hi T[k]) = (lr, li);
 // re = dot2(x, (lr, -li)), im = dot2(swap(x), (lr, li)).
-// LDS: plane granule G (8 samples) of plane pl sits in 16-B slot
-//   4p + ((2 pl + (G & 1)) ^ s(p)),  p = G >> 1,  s(p) = ((p>>2)&3) ^ 2((p>>1)&1):
-// no padding; the XOR spreads both access patterns over all 16 bank slots:
-// a ds_read_b128 group's lanes (granules 2t + c) and a ds_write2_b64 group's
-// 16 consecutive lanes (staged granules g -> 8-B halves) are conflict-free
-// (checked exhaustively; the padded 5-slot layout it replaces cost 2-way
-// write conflicts, SQ_LDS_BANK_CONFLICT 30.5 M per 2^28-sample launch).
+// LDS: the planes are stored column-major.  Plane granule G (8 samples of one
+// component, 16 B) of plane pl sits in slot  pl*2NC + (G&1)*NC + (G>>1)
+// (NC = 4 mod 8).  A lane's window reads (granule 2t + HG + c, c compile-time)
+// are then one per-lane base t plus an immediate offset -- no per-read
+// address arithmetic -- and the 16 lanes of a ds_read_b128 group hit 16
+// consecutive slots; the staging writes (staged granule g -> 8-B half g&1 of
+// plane granule g>>1) put 16 consecutive lanes on 16 distinct 8-B bank slots
+// because 2NC = 8 (mod 16).  No padding.  (The XOR-swizzled layout this
+// replaces needed ~6 VALU ops per read: ~200 per wave tile.)
+template <int NC>
 __device__ __forceinline__ int dot2_slot(int G, int pl) {
-    const int p = G >> 1;
-    return 4 * p + ((2 * pl + (G & 1)) ^ (((p >> 2) & 3) ^ (2 * ((p >> 1) & 1))));
+    static_assert(NC % 8 == 4, "2 NC = 8 (mod 16): conflict-free staging writes");
+    return pl * 2 * NC + (G & 1) * NC + (G >> 1);
 }
 __device__ __forceinline__ int32_t clamp_s14(int32_t v) {
     const int32_t a = v >> 14;  // |v| < 2^30: never INT_MIN
@@ -979,9 +982,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     constexpr int TG = (4 * TO + HS) / 4;         // staged 16-B sample granules
     constexpr int PER = ceildiv(TG, BLOCK);
     constexpr int PG = (4 * TO + HS) / 8;         // plane granules
-    constexpr int LSLOTS = 4 * ceildiv(PG, 2);
+    constexpr int NC0 = ceildiv(PG, 2);
+    constexpr int NC = NC0 + ((4 - NC0 % 8) + 8) % 8;  // slots per plane row, = 4 (mod 8)
+    constexpr int LSLOTS = 4 * NC;
     constexpr int TABMAX = MIX ? (TABM ? 8192 : 4096) : 1;
     static_assert(HS % 16 == 0 && 2 * (J - 1) <= HS, "halo geometry");
+    static_assert(HG % 2 == 0 && BLOCK % 16 == 0, "column-major plane layout");
     __shared__ uint4 lds[LSLOTS];
     __shared__ __attribute__((aligned(16))) uint32_t ctab[TABMAX];
 
@@ -1063,7 +1069,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     // staged granule g -> plane granule g>>1, half g&1
     auto lds_half = [&](int g, int plane) {
         const int G = g >> 1;
-        return (uint2 *)&lds[dot2_slot(G, plane)] + (g & 1);
+        return (uint2 *)&lds[dot2_slot<NC>(G, plane)] + (g & 1);
     };
     auto put = [&](int g, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
         *lds_half(g, 0) = make_uint2(lo16_pair(w0, w1), lo16_pair(w2, w3));
@@ -1194,8 +1200,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
         uint32_t Dr[OFF + 8], Di[OFF + 8];
         auto load_g = [&](int c) {  // plane granule lb + c -> dwords d = 4c .. 4c+3
             typedef uint32_t u4v_t __attribute__((ext_vector_type(4)));
-            u4v_t gr = *(const u4v_t *)&lds[dot2_slot(lb + c, 0)];
-            u4v_t gi = *(const u4v_t *)&lds[dot2_slot(lb + c, 1)];
+            // granule lb + c = 2t + HG + c: row c & 1, column t + (HG + c) >> 1
+            const int o = (c & 1) * NC + ((HG + c) >> 1);
+            u4v_t gr = *(const u4v_t *)&lds[t + o];
+            u4v_t gi = *(const u4v_t *)&lds[t + o + 2 * NC];
             // keep every read a whole ds_read_b128: at the window edges the
             // compiler would load only the words used, as ds_read2_b32 /
             // ds_read_b96, whose 4-B lane groups the layout does not spread
