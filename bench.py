@@ -259,7 +259,8 @@ class UpWorkload(Workload):
     dtype = "i32"
     bytes_per_sample = 20.0  # 4 B complex<int16_t> in, 4 x 4 B out per input sample
     # 4 outputs per input, 32 taps each, 2 components: 256 int MACs = 128 v_dot2
-    # lane-ops per input sample (algorithmic; the kernel issues 136)
+    # lane-ops per input sample (the kernel issues exactly these: 16 tap pairs
+    # (c[2p+1], c[2p]) per phase and component)
     dot2_per_sample = 128.0
 
     def __init__(self, S, torch, L, channels, rank, fp):

@@ -207,25 +207,33 @@ __global__ __launch_bounds__(kUpBlock) void up_tile(const uint32_t *in, long n_i
 
 // Tiled polyphase interpolator on v_dot2_i32_i16 (variant 0 with int16-range
 // taps, LR in {2, 4}).  Each lane owns RD = 8 consecutive input samples.  Taps
-// of phase o are paired P_p = (lo c_o[2p], hi c_o[2p-1]); the pair of input j
-// reads the packed samples (x[j-2p], x[j-2p+1]), which for even j is dword
-// (j-2p)/2 of an even-aligned plane E[e] = (x[2e], x[2e+1]) and for odd j dword
-// (j-1-2p)/2 of an odd-aligned plane O[e] = (x[2e+1], x[2e+2]).  A lane's 8
-// inputs read E[4t'+r/2-p] / O[4t'+(r-1)/2-p]: one 4-dword register window per
-// plane and component sliding one dword per pair, one ds_read_b128 per plane
-// every 4 pairs.  int16 x int16 -> int32 products, wrap-around accumulate:
-// exactly the reference's complex<int32_t> arithmetic.
+// of phase o are paired Q_p = (lo c_o[2p+1], hi c_o[2p]) (c_o[H] = 0), p <
+// ceil(H/2); the pair of input j multiplies the packed samples (x[j-2p-1],
+// x[j-2p]), which for even j = 2m is dword m-p-1 of an odd-aligned plane
+// O[e] = (x[2e+1], x[2e+2]) and for odd j = 2m+1 dword m-p of an even-aligned
+// plane E[e] = (x[2e], x[2e+1]).  A lane's 8 inputs read O[4t'+r/2-1-p] (even
+// r) / E[4t'+(r-1)/2-p] (odd r): one 4-dword register window per plane and
+// component sliding one dword per pair, one ds_read_b128 per plane every 4
+// pairs.  ceil(H/2) dot2 per phase and component (the (c[2p], c[2p-1])
+// pairing needed H/2 + 1).  int16 x int16 -> int32 products, wrap-around
+// accumulate: exactly the reference's complex<int32_t> arithmetic.
 constexpr int kUpRD = 8, kUpBlockD = 256;
 
-template <int LR, bool NTS = false>
-__global__ __launch_bounds__(kUpBlockD) void up_tile_dot2(const uint32_t *in, long n_in, long n_total,
+// WS: window register sets (3: the next granule is read a chunk ahead, 150
+// VGPRs at LR = 4; 2: it is read at the end of the chunk into the set that
+// chunk is done with, <= 128 VGPRs -> 4 waves per SIMD); MINW as launch bound
+// PPC: pairs per phase as a compile-time constant (0: runtime, from H): the
+// chunk loop unrolls completely, the window sets rotate without register
+// copies and each accumulator starts with a dot2 into an inline 0.
+template <int LR, bool NTS = false, int WS = 3, int MINW = 1, int PPC = 0>
+__global__ __launch_bounds__(kUpBlockD, MINW) void up_tile_dot2(const uint32_t *in, long n_in, long n_total,
                                                          const uint32_t *hist_in, uint32_t *hist_out,
                                                          const uint32_t *pairs, int H, unsigned shift, uint32_t *out) {
     constexpr int R = kUpRD, TI = R * kUpBlockD;
     extern __shared__ uint4 ug[];  // 4 planes (E_re, E_im, O_re, O_im) of PGR granules each
     const int Hm1 = H - 1;
-    const int PP = H / 2 + 1;            // pairs per phase
-    const int HG = (PP + 3) / 4;         // halo granules per plane (window reach)
+    const int PP = PPC ? PPC : (H + 1) / 2;  // pairs per phase
+    const int HG = (PP + 3) / 4;         // halo granules per plane (window reach: dword D0 - PP)
     const int PGR = TI / 8 + HG;         // granules per plane (4 dwords = 8 samples)
     const int t = threadIdx.x;
     if (blockIdx.x == 0) {
@@ -259,15 +267,18 @@ __global__ __launch_bounds__(kUpBlockD) void up_tile_dot2(const uint32_t *in, lo
     }
     __syncthreads();
     // lane base: input j0 + 8t = plane dword D0 = 4t + 4*HG (granule gb).  Input
-    // r, pair p reads dword D0 + k - p, k = r/2 (plane E for even r, O for odd):
+    // r, pair p reads dword D0 + k - p, k = r/2 - 1 in plane O for even r,
+    // k = (r-1)/2 in plane E for odd r:
     // for the chunk of pairs 4q..4q+3 those are dwords of granules gb - q
     // (`cur`) and gb - q - 1 (`nxt`), two register sets that swap roles.
     const int gb = t + HG;
     int32_t yr[LR][R], yi[LR][R];
+    if constexpr (PPC == 0) {
 #pragma unroll
-    for (int o = 0; o < LR; ++o)
+        for (int o = 0; o < LR; ++o)
 #pragma unroll
-        for (int r = 0; r < R; ++r) yr[o][r] = yi[o][r] = 0;
+            for (int r = 0; r < R; ++r) yr[o][r] = yi[o][r] = 0;
+    }
     ConstPtr<uint32_t> tp = const_view<uint32_t>(pairs);
     // Three window register sets rotate over the chunks and the taps of a
     // chunk (4 pairs x LR phases, contiguous: dword (4q + pp) LR + o) arrive in
@@ -295,40 +306,68 @@ __global__ __launch_bounds__(kUpBlockD) void up_tile_dot2(const uint32_t *in, lo
         for (int pp = 0; pp < 4; ++pp) {
             const int p = 4 * q + pp;
             if (p >= PP) break;  // the last chunk only
-            if (pp == 1 && q + 1 < NQ) {
+            if (WS == 3 && pp == 1 && q + 1 < NQ) {
                 load(nn, gb - q - 2);
                 load_taps(Tn, q + 1);
             }
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const int k = r >> 1, rel = k - pp;  // -3..3
-                const int pr = (r & 1) ? 2 : 0, pi = pr + 1;  // planes E_re/E_im or O_re/O_im
+                const int k = (r & 1) ? (r >> 1) : (r >> 1) - 1, rel = k - pp;  // -4..3
+                const int pr = (r & 1) ? 0 : 2, pi = pr + 1;  // planes E_re/E_im or O_re/O_im
                 const uint32_t xr = rel >= 0 ? cur[pr][rel] : nxt[pr][rel + 4];
                 const uint32_t xi = rel >= 0 ? cur[pi][rel] : nxt[pi][rel + 4];
 #pragma unroll
                 for (int o = 0; o < LR; ++o) {
                     const uint32_t P = Tc[pp * LR + o];
-                    yr[o][r] = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t_u, xr),
-                                                      __builtin_bit_cast(short2_t_u, P), yr[o][r], false);
-                    yi[o][r] = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t_u, xi),
-                                                      __builtin_bit_cast(short2_t_u, P), yi[o][r], false);
+                    if (PPC && q == 0 && pp == 0) {  // first pair: into an inline 0
+                        asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(yr[o][r]) : "v"(xr), "s"(P));
+                        asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(yi[o][r]) : "v"(xi), "s"(P));
+                    } else {
+                        yr[o][r] = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t_u, xr),
+                                                          __builtin_bit_cast(short2_t_u, P), yr[o][r], false);
+                        yi[o][r] = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t_u, xi),
+                                                          __builtin_bit_cast(short2_t_u, P), yi[o][r], false);
+                    }
                 }
             }
         }
+        if constexpr (WS == 3) {
 #pragma unroll
-        for (int i = 0; i < TPC; ++i) Tc[i] = Tn[i];
+            for (int i = 0; i < TPC; ++i) Tc[i] = Tn[i];
+        }
     };
     load(W0, gb);
     load(W1, gb - 1);
     load_taps(Tc, 0);
     int q = 0;
-    for (; q + 3 <= NQ; q += 3) {
-        chunk(q, W0, W1, W2);
-        chunk(q + 1, W1, W2, W0);
-        chunk(q + 2, W2, W0, W1);
+    if constexpr (WS == 3) {
+#pragma unroll
+        for (; q + 3 <= NQ; q += 3) {
+            chunk(q, W0, W1, W2);
+            chunk(q + 1, W1, W2, W0);
+            chunk(q + 2, W2, W0, W1);
+        }
+        if (q < NQ) chunk(q, W0, W1, W2);
+        if (q + 1 < NQ) chunk(q + 1, W1, W2, W0);
+    } else {
+        // chunk q reads granules gb-q (cur) and gb-q-1 (nxt); the next chunk's
+        // new granule gb-q-2 goes into cur once this chunk is done with it
+        (void)W2;
+        auto chunk2 = [&](int qq, uint32_t (&cur)[4][4], const uint32_t (&nxt)[4][4]) {
+            uint32_t none[4][4];
+            chunk(qq, cur, nxt, none);  // no early read (nn unused when WS == 2)
+            if (qq + 1 < NQ) {
+                load(cur, gb - qq - 2);
+                load_taps(Tc, qq + 1);
+            }
+        };
+#pragma unroll
+        for (; q + 2 <= NQ; q += 2) {
+            chunk2(q, W0, W1);
+            chunk2(q + 1, W1, W0);
+        }
+        if (q < NQ) chunk2(q, W0, W1);
     }
-    if (q < NQ) chunk(q, W0, W1, W2);
-    if (q + 1 < NQ) chunk(q + 1, W1, W2, W0);
     // outputs -> LDS (lane chunk of 8*LR words at a 9-granule stride for LR = 4,
     // conflict-free) -> whole-line 16-B stores of the tile's contiguous output
     constexpr int GPLo = R * LR / 4;    // output granules per lane
@@ -406,14 +445,14 @@ static int up_set(srcdsp_up_state &u, const void *coeffs, int n) {
     if (u.coef_i16) {  // tap pairs of each phase: (lo c_o[2p], hi c_o[2p-1]), c_o[-1] = c_o[H] = 0
         // chunk-major for up_tile_dot2: the 4 pairs x L phases of chunk q are
         // the contiguous dwords [4qL, 4(q+1)L), pair p of phase o at p L + o,
-        // zero-padded to whole chunks
-        const int Hh = n / (int)u.L, PP = Hh / 2 + 1, NQ = (PP + 3) / 4;
+        // zero-padded to whole chunks; pair p = (lo c_o[2p+1], hi c_o[2p])
+        const int Hh = n / (int)u.L, PP = (Hh + 1) / 2, NQ = (PP + 3) / 4;
         std::vector<uint32_t> pr((size_t)u.L * 4 * NQ, 0u);
         auto tap = [&](unsigned o, int i) {
             return (i >= 0 && i < Hh) ? (uint32_t)(uint16_t)(int16_t)c[o + (size_t)i * u.L] : 0u;
         };
         for (unsigned o = 0; o < u.L; ++o)
-            for (int q = 0; q < PP; ++q) pr[(size_t)q * u.L + o] = tap(o, 2 * q) | (tap(o, 2 * q - 1) << 16);
+            for (int q = 0; q < PP; ++q) pr[(size_t)q * u.L + o] = tap(o, 2 * q + 1) | (tap(o, 2 * q) << 16);
         SRCDSP_HIP_TRY(hipMalloc(&u.d_pair, 4 * pr.size()));
         SRCDSP_HIP_TRY(hipMemcpy(u.d_pair, pr.data(), 4 * pr.size(), hipMemcpyHostToDevice));
     }
@@ -458,18 +497,28 @@ static int up_launch(srcdsp_up_state &u, const void *d_in, size_t n_in, void *d_
     if (tiled && u.variant == UV_CI16_I32 && u.coef_i16 && (u.L == 2 || u.L == 4) &&
         ((uintptr_t)d_out & 15u) == 0) {
         constexpr int TI = kUpRD * kUpBlockD;
-        const int PP = u.H / 2 + 1, HG = (PP + 3) / 4, PGR = TI / 8 + HG;
+        const int PP = (u.H + 1) / 2, HG = (PP + 3) / 4, PGR = TI / 8 + HG;
         const size_t out_lds = 16 * (size_t)kUpBlockD * (kUpRD * u.L / 4 + 1);  // staged output tile
         const size_t smem = std::max(4 * 16 * (size_t)PGR, out_lds);
         const dim3 grid((unsigned)((n_total + TI - 1) / TI));
         // non-temporal output stores: 0.414 -> 0.385 ms at L = 4, 128 taps, 2^26 inputs
 #define SRCDSP_UP_DOT2(LR)                                                                                        \
-    hipLaunchKernelGGL((up_tile_dot2<LR, true>), grid, dim3(kUpBlockD), smem, s, (const uint32_t *)d_in, (long)n_in, \
+    hipLaunchKernelGGL((up_tile_dot2<LR, true, WSV, MW, PPV>), grid, dim3(kUpBlockD), smem, s, (const uint32_t *)d_in, (long)n_in, \
                        n_total, (const uint32_t *)hin0, (uint32_t *)hout0, u.d_pair, u.H, shift, (uint32_t *)d_out)
-        if (u.L == 2)
+        // 32 taps per phase (L = 4 x 128 taps, L = 2 x 64): a compile-time shape
+        if (u.L == 2 && PP == 16) {
+            constexpr int WSV = 3, MW = 1, PPV = 16;
             SRCDSP_UP_DOT2(2);
-        else
+        } else if (u.L == 4 && PP == 16) {
+            constexpr int WSV = 3, MW = 1, PPV = 16;
             SRCDSP_UP_DOT2(4);
+        } else if (u.L == 2) {
+            constexpr int WSV = 3, MW = 1, PPV = 0;
+            SRCDSP_UP_DOT2(2);
+        } else {
+            constexpr int WSV = 3, MW = 1, PPV = 0;
+            SRCDSP_UP_DOT2(4);
+        }
 #undef SRCDSP_UP_DOT2
         SRCDSP_HIP_TRY(hipGetLastError());
         u.cur ^= 1;
