@@ -77,6 +77,8 @@ def main():
             res[c] = sum(vals) / len(vals)
         res["dispatches"] = len(rows)
     L = a.samples - a.samples % 4
+    if a.workload == "up":
+        L //= 4  # bench.py's up workload takes samples/4 inputs (4x as many outputs)
     read_b = 2.0 * res["FETCH_SIZE"] * 1024.0      # gfx950 FETCH_SIZE half-count correction
     write_b = res["WRITE_SIZE"] * 1024.0
     alg = BYTES_PER_SAMPLE[a.workload] * L
