@@ -123,6 +123,23 @@ __global__ __launch_bounds__(256) void burst_probe(const float4_t *in, float4_t 
     }
 }
 
+// 1:2 expansion (the float -> complex<float> FilterFir stream: 4 B read, 8 B
+// written per sample): each lane reads one granule and writes two; a wave's
+// stores cover 2 KiB contiguous.  n_in = input granules.
+template <bool NTL, bool NTS>
+__global__ __launch_bounds__(256) void expand_probe(const float4_t *in, float4_t *out, long n_in) {
+    const long nth = (long)gridDim.x * 256;
+    const int t = threadIdx.x;
+    for (long base = (long)blockIdx.x * 256; base < n_in; base += nth) {
+        const float4_t v = ld<NTL>(in + base + t);
+        // the wave's input granules base + (t & ~63) .. +63 -> its output granules
+        // 2 (base + (t & ~63)) .. +127; lane l writes l and 64 + l of them
+        const long w0 = 2 * (base + (t & ~63)) + (t & 63);
+        st<NTS>(out + w0, v);
+        st<NTS>(out + w0 + 64, v * 2.f);
+    }
+}
+
 __global__ __launch_bounds__(256) void fill_probe(float4_t *out, long n) {
     const long nth = (long)gridDim.x * 256;
     const float4_t z = {1, 2, 3, 4};
@@ -164,6 +181,15 @@ extern "C" int bw_probe(int id, int blocks, const void *in_, void *out_, long n_
         ACASE(120, 1, 2) ACASE(121, 3, 2) ACASE(122, 16, 2) ACASE(123, 17, 2) ACASE(124, 18, 2) ACASE(125, 19, 2)
     case 20:
         hipLaunchKernelGGL(fill_probe, dim3(blocks), dim3(256), 0, s, out, n_in16 / 4);
+        break;
+    case 30:  // 1:2 expansion over n_in16 / 2 input granules (output = n_in16 granules)
+        hipLaunchKernelGGL((expand_probe<false, false>), dim3(blocks), dim3(256), 0, s, in, out, n_in16 / 2);
+        break;
+    case 31:
+        hipLaunchKernelGGL((expand_probe<true, true>), dim3(blocks), dim3(256), 0, s, in, out, n_in16 / 2);
+        break;
+    case 32:
+        hipLaunchKernelGGL((expand_probe<false, true>), dim3(blocks), dim3(256), 0, s, in, out, n_in16 / 2);
         break;
         CASE(13, 4, 2, true, true, true)    // 4:1 contiguous, nt both
 #define BCASE(id, K, NL, NS)                                                                          \

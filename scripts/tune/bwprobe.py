@@ -35,6 +35,11 @@ def main():
         for k, la in enumerate((1, 3, 16, 17, 18, 19)):
             CASES[120 + k] = (f"4:1 contig ld aux {la} st aux 2", 4)
         grids = (1024, 2048)
+    if os.environ.get("BW_EXPAND"):
+        CASES.clear()
+        CASES.update({30: ("1:2 expand", -2), 31: ("1:2 expand nt-both", -2), 32: ("1:2 expand nt-store", -2),
+                      0: ("copy 1:1", 1), 20: ("write-only fill", -1), 10: ("read-only U2 nt", 0)})
+        grids = (1024, 2048, 4096, 8192)
     if os.environ.get("BW_BURST"):
         CASES.clear()
         CASES.update({13: ("4:1 contig U2 nt-both", 4), 5: ("4:1 gs U2 nt-both", 4),
@@ -63,6 +68,8 @@ def main():
             byt = n16 * 16 + n16 // ratio * 16
         elif ratio == 0:
             byt = n16 * 16
+        elif ratio == -2:  # 1:2 expansion: n16/2 granules read, n16 written
+            byt = n16 // 2 * 16 + n16 * 16
         else:
             byt = n16 // 4 * 16
         row = []
