@@ -596,7 +596,8 @@ def pmc_traffic(args, work_name, per_launch_samples):
     """Per-launch HBM bytes from the committed rocprofv3 PMC summary (see
     profiles/README.md for how it is collected and corrected), if it was
     measured on this launch size AND on the current kernel sources (its
-    `kernel_sources_sha` against srcdsp_amd.build.source_digest()).  Returns
+    `kernel_sources_sha` against srcdsp_amd.build.source_digest(workload):
+    the translation unit of the kernel and its headers).  Returns
     (bytes or None, note)."""
     from srcdsp_amd.build import source_digest
     try:
@@ -607,7 +608,7 @@ def pmc_traffic(args, work_name, per_launch_samples):
     e = t.get(work_name)
     if not e or int(e.get("samples_per_launch", -1)) != per_launch_samples:
         return None, "no PMC summary for this workload size"
-    if e.get("kernel_sources_sha") != source_digest():
+    if e.get("kernel_sources_sha") != source_digest(args.workload):
         print(f"bench: WARNING {args.traffic_json} entry {work_name} predates the current kernel sources; "
               "traffic not reported (re-run scripts/pmc_traffic.py)", file=sys.stderr, flush=True)
         return None, "stale: PMC summary predates the current kernel sources"

@@ -87,7 +87,7 @@ def main():
              "algorithmic_bytes_per_launch": int(alg), "traffic_over_algorithmic": (read_b + write_b) / alg,
              "raw_counters_per_launch": res,
              "correction": "read = 2*FETCH_SIZE*1024 (gfx950 half-count), write = WRITE_SIZE*1024",
-             "kernel_sources_sha": source_digest()}
+             "kernel_sources_sha": source_digest(a.workload)}
     if "SQ_WAVE_CYCLES" in res and res.get("SQ_WAVE_CYCLES"):
         entry["valu_active_frac_of_wave_cycles"] = res["SQ_ACTIVE_INST_VALU"] / res["SQ_WAVE_CYCLES"]
         entry["wait_any_frac"] = res["SQ_WAIT_ANY"] / res["SQ_WAVE_CYCLES"]

@@ -42,13 +42,44 @@ def _headers() -> list[str]:
     return glob.glob(os.path.join(CSRC, "*.h")) + [os.path.join(ROOT, "include", "srcdsp_hip.h")]
 
 
-def source_digest() -> str:
-    """sha256 (16 hex) over the kernel sources (csrc/*.hip, csrc/*.h and the C
-    ABI header): stamps measured evidence (profiles/pmc_traffic.json) with the
-    code it was measured on, so a later kernel change shows it as stale."""
+# the translation unit that holds each bench workload's dominant kernel
+WORKLOAD_TU = {"decim": "decim.hip", "mixdecim": "decim.hip", "ci16decim": "decim.hip", "fir": "decim.hip",
+               "up": "upsamp.hip", "corr": "corr.hip", "fifo": "fifo.hip", "iq": "fifo.hip"}
+
+
+def _tu_files(tu: str) -> list[str]:
+    """`tu` and every local header it reaches through #include "..." (csrc/, include/)."""
+    seen, todo = [], [os.path.join(CSRC, tu)]
+    while todo:
+        f = todo.pop()
+        if f in seen or not os.path.exists(f):
+            continue
+        seen.append(f)
+        with open(f) as fh:
+            for line in fh:
+                line = line.strip()
+                if line.startswith("#include \""):
+                    name = line.split('"')[1]
+                    for d in (os.path.dirname(f), CSRC, os.path.join(ROOT, "include")):
+                        if os.path.exists(os.path.join(d, name)):
+                            todo.append(os.path.normpath(os.path.join(d, name)))
+                            break
+    return seen
+
+
+def source_digest(workload: str | None = None) -> str:
+    """sha256 (16 hex) over kernel sources: stamps measured evidence
+    (profiles/pmc_traffic.json) with the code it was measured on, so a later
+    change shows it as stale.  With a bench workload: only the translation
+    unit of its kernel and the headers that unit includes; without one: every
+    csrc/*.hip, csrc/*.h and the C ABI header."""
     import hashlib
     h = hashlib.sha256()
-    for f in sorted(glob.glob(os.path.join(CSRC, "*.hip")) + _headers()):
+    if workload is not None:
+        files = sorted(_tu_files(WORKLOAD_TU[workload]))
+    else:
+        files = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + _headers())
+    for f in files:
         h.update(os.path.basename(f).encode())
         with open(f, "rb") as fh:
             h.update(fh.read())

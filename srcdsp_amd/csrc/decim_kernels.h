@@ -795,6 +795,11 @@ __device__ __forceinline__ void mix_dot2(uint32_t w, uint32_t C, int32_t &re, in
 // so the image has the cf32 layout: LDS blocks are 8 granules + one pad
 // granule and the lanes' ds_read_b128 are conflict-free.  One tile per
 // workgroup; the image holds ceil(N/16) halo blocks before the tile.
+__device__ __forceinline__ float4 nt_load4(const float4 *p) {
+    typedef float f4_t __attribute__((ext_vector_type(4)));
+    const f4_t w = __builtin_nontemporal_load((const f4_t *)p);
+    return make_float4(w[0], w[1], w[2], w[3]);
+}
 constexpr int kDtBlock = 256, kDtMaxTaps = 1024;
 // samples per lane block: a multiple of M and of 4 (an even number of 16-B
 // granules, so the padded block stride RM/2 + 1 is odd: conflict-free reads)
@@ -837,8 +842,11 @@ __global__ __launch_bounds__(kDtBlock) void decim_tile(DecimLaunch a) {
 #pragma unroll
         for (int i = 0; i < RM / 2; ++i) {
             const long s = s0 + 2L * (G0 + t + i * kDtBlock);
+            // complex<float>: non-temporal, the body is read once (the halo
+            // re-read is an L2 hit): 4 % at M = 2/4 x 63 taps; complex<int16_t>
+            // measured 0-5 % slower with it (profiles/tuning/r02_tile_nt_ab.txt)
             if constexpr (CF) {
-                v[i] = *(const float4 *)(in + s);
+                v[i] = nt_load4((const float4 *)(in + s));
             } else {
                 const uint2 w = *(const uint2 *)(in + s);
                 v[i] = split(w.x, w.y);
@@ -937,8 +945,8 @@ __global__ __launch_bounds__(kDtBlock) void decim_tile(DecimLaunch a) {
         if (R % 2 == 0 && o0 + R <= a.n_out) {
 #pragma unroll
             for (int r = 0; r + 1 < R; r += 2)
-                *(float4 *)(out + o0 + r) = make_float4(q16f(yr[r], a.shift), q16f(yi[r], a.shift),
-                                                        q16f(yr[r + 1], a.shift), q16f(yi[r + 1], a.shift));
+                store16<true>((float4 *)(out + o0 + r), make_float4(q16f(yr[r], a.shift), q16f(yi[r], a.shift),
+                                                                    q16f(yr[r + 1], a.shift), q16f(yi[r + 1], a.shift)));
         } else {
 #pragma unroll
             for (int r = 0; r < R; ++r)

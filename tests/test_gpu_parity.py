@@ -124,6 +124,38 @@ def test_decim_ci16_any_taps_tile_vs_oracle(S, O, kind, M, ntaps):
         assert np.array_equal(g.step(dev(xs)).cpu().numpy(), r.step(xs)), (off, n)
 
 
+@pytest.mark.parametrize("kind,M,ntaps", [("cf32", 2, 63), ("cf32", 4, 63), ("cf32", 3, 95), ("cf32", 8, 1000),
+                                          ("cf32", 4, 600), ("i24", 4, 63), ("t16", 2, 127), ("i16", 5, 61),
+                                          ("i32", 16, 300)])
+def test_decim_tile_persistent_many_tiles_vs_oracle(S, O, kind, M, ntaps):
+    """decim_tile is persistent (grid = twice the resident workgroups): calls
+    of 2^23-2^24 samples give every workgroup several tiles, so the prefetch
+    loop, the grid-stride tile order, the N > 512 halo path (600 and 1000 taps)
+    and a ragged last tile all run; chained calls carry the history."""
+    rng = np.random.default_rng(M * 7 + ntaps)
+    total = (1 << 24) + 3 * M * 1000 + 5 * M
+    if kind == "cf32":
+        c = (rng.standard_normal(ntaps) / max(2, ntaps) ** 0.5).astype(np.float32)
+        x = O["fma"].gen_cf32(99 + ntaps, M, 0, total)
+        g = S.FilterDnsamplingFir(c, M, fp="fma")
+        r = O["fma"].decim(0, M, c)
+    else:
+        lim = {"i16": 32767, "i24": (1 << 23) - 1, "i32": 1 << 24, "t16": 32767}[kind]
+        c = rng.integers(-lim, lim + 1, size=ntaps).astype(np.int32)
+        x = O["strict"].gen_ci16(5 + ntaps, M, 0, total, -32768, 32767)
+        if kind == "t16":
+            c = c.astype(np.int16)
+            g = S.FilterDnsamplingFir(c, M, "complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int16_t")
+            r = O["strict"].decim(2, M, c)
+        else:
+            g = S.FilterDnsamplingFir(c, M, "complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int32_t")
+            r = O["strict"].decim(1, M, c)
+    for off, n in _chunks(len(x), [1 << 23, (1 << 23) + 3 * M * 1000, 5 * M]):
+        n -= n % M
+        xs = x[off:off + n]
+        assert np.array_equal(g.step(dev(xs)).cpu().numpy(), r.step(xs)), (off, n)
+
+
 @pytest.mark.parametrize("kind", ["i16", "i24", "i32"])
 @pytest.mark.parametrize("ntaps", [1, 16, 17, 31, 100, 1024])
 def test_fir_ci16_tile_vs_oracle(S, O, kind, ntaps):
