@@ -127,11 +127,11 @@ def test_decim_ci16_any_taps_tile_vs_oracle(S, O, kind, M, ntaps):
 @pytest.mark.parametrize("kind,M,ntaps", [("cf32", 2, 63), ("cf32", 4, 63), ("cf32", 3, 95), ("cf32", 8, 1000),
                                           ("cf32", 4, 600), ("i24", 4, 63), ("t16", 2, 127), ("i16", 5, 61),
                                           ("i32", 16, 300)])
-def test_decim_tile_persistent_many_tiles_vs_oracle(S, O, kind, M, ntaps):
-    """decim_tile is persistent (grid = twice the resident workgroups): calls
-    of 2^23-2^24 samples give every workgroup several tiles, so the prefetch
-    loop, the grid-stride tile order, the N > 512 halo path (600 and 1000 taps)
-    and a ragged last tile all run; chained calls carry the history."""
+def test_decim_tile_large_calls_vs_oracle(S, O, kind, M, ntaps):
+    """decim_tile on calls of 2^23-2^24 samples (thousands of tiles, more
+    workgroups than the chip holds at once), long halos (600 and 1000 taps),
+    a ragged last tile and a call shorter than the filter; chained calls carry
+    the history.  Bit-exact against the oracle on every output."""
     rng = np.random.default_rng(M * 7 + ntaps)
     total = (1 << 24) + 3 * M * 1000 + 5 * M
     if kind == "cf32":
