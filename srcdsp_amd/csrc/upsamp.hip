@@ -291,8 +291,14 @@ __global__ __launch_bounds__(kUpBlockD, MINW) void up_tile_dot2(const uint32_t *
     auto load = [&](uint32_t (&w)[4][4], int gi) {
 #pragma unroll
         for (int pl4 = 0; pl4 < 4; ++pl4) {
-            const uint4 v = ug[pl4 * PGR + gi];
-            w[pl4][0] = v.x; w[pl4][1] = v.y; w[pl4][2] = v.z; w[pl4][3] = v.w;
+            typedef uint32_t u4v_t __attribute__((ext_vector_type(4)));
+            // volatile keeps every window read a whole ds_read_b128
+            // (conflict-free at the lanes' 16-B stride): at the window's far end
+            // the compiler would read only the dwords used, as ds_read_b32 /
+            // ds_read2_b32, whose 32-lane groups at a 16-B stride hit 8 banks
+            typedef const volatile __attribute__((address_space(3))) u4v_t *lds_u4v;
+            const u4v_t v = *(lds_u4v)(&ug[pl4 * PGR + gi]);
+            w[pl4][0] = v[0]; w[pl4][1] = v[1]; w[pl4][2] = v[2]; w[pl4][3] = v[3];
         }
     };
     auto load_taps = [&](uint32_t (&T)[TPC], int q) {
