@@ -710,6 +710,8 @@ def main():
                 "frac": round(tops / VALU_PEAK_TOPS, 4), "traffic": None, "kernel": work.name,
                 "kernel_ms": round(kern_avg_ms, 4), "dot2_per_input_sample": dps}
         if valu["frac"] > roof["frac"]:
+            # HBM bytes per launch are the kernel's traffic whichever bound binds
+            valu.update(traffic=roof["traffic"], traffic_source=roof.get("traffic_source"))
             roof, other = valu, roof
         else:
             other = valu
