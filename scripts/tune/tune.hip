@@ -3,6 +3,7 @@
 // so they can be timed side by side, interleaved, in one process.
 #include "../../srcdsp_amd/csrc/decim_kernels.h"
 #include "decim_mfma.h"
+#include "decim_ring.h"
 
 using namespace srcdsp;
 
@@ -197,6 +198,20 @@ extern "C" int tune_decim(int variant, int grid, const float *d_coef, const void
     case 409: L.ntiles = tiles(256); return launch(decim_wave_cf32<127, 512, true, 4, true, 0, 2, true>, grid, 512, L, s);
     case 75: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, 0, true, true>, grid, 512, L, s);
     case 24: L.ntiles = tiles(128 * 8); return launch(decim_stream2_cf32<127, 8, 128, true, 2, true>, grid, 128, L, s);
+    // LDS-DMA loader/consumer ring (decim_ring.h): one workgroup per CU (grid 256 whatever is asked),
+    // <NCONS consumer waves, NSLOT slots, NPF slots in flight, CH wave tiles per chunk>; whole chunks only
+#define RING(V, NC, NS, NP, CHK)                                                                  \
+    case V:                                                                                       \
+        if (L.n_out % (256L * 256 * CHK)) return -2;                                              \
+        L.ntiles = L.n_out / 256;                                                                 \
+        return launch(decim_ring_cf32<NC, NS, NP, CHK>, 256, 64 * (NC + 1), L, s);
+    RING(500, 12, 15, 3, 8)
+    RING(501, 12, 15, 2, 8)
+    RING(502, 10, 15, 4, 8)
+    RING(503, 12, 15, 3, 1)
+    RING(504, 8, 15, 5, 8)
+    RING(505, 12, 15, 3, 32)
+#undef RING
     default: return -1;
     }
 }
