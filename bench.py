@@ -605,7 +605,8 @@ def pmc_traffic(args, work_name, per_launch_samples):
             t = json.load(f)
     except Exception:
         return None, "no PMC summary"
-    e = t.get(work_name)
+    ch = args.channels_per_gpu if args.workload == "decim" else 1
+    e = t.get(work_name + (f"x{ch}" if ch > 1 else ""))  # a batched launch has its own entry
     if not e or int(e.get("samples_per_launch", -1)) != per_launch_samples:
         return None, "no PMC summary for this workload size"
     if e.get("kernel_sources_sha") != source_digest(args.workload):

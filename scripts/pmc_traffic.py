@@ -62,10 +62,13 @@ def main():
     ap.add_argument("--workload", default="decim")
     ap.add_argument("--tag", default="latest")
     ap.add_argument("--samples", type=int, default=1 << 28)
+    ap.add_argument("--channels", type=int, default=1, help="decim only: channels per launch (config 3's share: 8)")
     a = ap.parse_args()
     key = KERNEL_KEYS[a.workload]
     bench_args = ["--workload", a.workload, "--steps", "5", "--warmup", "1", "--no-cpu-baseline", "--no-pcie",
                   "--samples", str(a.samples)]
+    if a.channels > 1:
+        bench_args += ["--channels-per-gpu", str(a.channels)]
     res = {}
     for i, counters in enumerate(PASSES):
         per = run_pass(counters, os.path.join(ROOT, "gpurun_out", f"pmc_{a.workload}_{i}"), bench_args)
@@ -76,7 +79,7 @@ def main():
             vals = [r[c] for r in rows if c in r]
             res[c] = sum(vals) / len(vals)
         res["dispatches"] = len(rows)
-    L = a.samples - a.samples % 4
+    L = (a.samples - a.samples % 4) * a.channels
     if a.workload == "up":
         L //= 4  # bench.py's up workload takes samples/4 inputs (4x as many outputs)
     read_b = 2.0 * res["FETCH_SIZE"] * 1024.0      # gfx950 FETCH_SIZE half-count correction
@@ -94,8 +97,9 @@ def main():
     # written under gpurun_out/ (what the GPU box hands back); copied into
     # profiles/ (tracked) by hand after review
     out = os.path.join(ROOT, "gpurun_out")
-    with open(os.path.join(out, f"pmc_{a.workload}_{a.tag}.json"), "w") as f:
-        json.dump({NAMES[a.workload]: entry}, f, indent=1)
+    key = NAMES[a.workload] + (f"x{a.channels}" if a.channels > 1 else "")
+    with open(os.path.join(out, f"pmc_{a.workload}{'x%d' % a.channels if a.channels > 1 else ''}_{a.tag}.json"), "w") as f:
+        json.dump({key: entry}, f, indent=1)
     print(json.dumps(entry, indent=1))
 
 
