@@ -396,7 +396,14 @@ __global__ __launch_bounds__(kUpBlockD, MINW) void up_tile_dot2(const uint32_t *
 #pragma unroll
     for (int i = 0; i < GPLo; ++i) {
         const int G = i * kUpBlockD + t;          // output granule within the tile
-        const uint4 v = ob[(G / GPLo) * STR + (G % GPLo)];
+        // one whole ds_read_b128 (volatile: the compiler split this read into
+        // ds_read_b32 / ds_read2_b32 for the partial-tile branch below, whose
+        // 32-lane groups at a 16-B stride hit 8 banks: 25 M conflict cycles
+        // per launch at L = 4, 2^26 inputs)
+        typedef uint32_t o4v_t __attribute__((ext_vector_type(4)));
+        typedef const volatile __attribute__((address_space(3))) o4v_t *lds_o4v;
+        const o4v_t vv4 = *(lds_o4v)(&ob[(G / GPLo) * STR + (G % GPLo)]);
+        const uint4 v = make_uint4(vv4[0], vv4[1], vv4[2], vv4[3]);
         const long w0 = wbase + 4L * G;
         if (w0 + 4 <= wend) {
             if constexpr (NTS) {  // streaming store: the output is written once, 4L x the input bytes
