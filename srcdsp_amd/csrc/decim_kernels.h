@@ -1305,12 +1305,22 @@ __device__ __forceinline__ void fir_lane(const float4 *fl, int gb, int N, ConstP
         y2[r] = (f2_t){0.f, 0.f};
     }
     S A[4], B[4], C[4];
+    // window reads through a volatile LDS view: every one a whole
+    // ds_read_b128 (conflict-free at the odd granule stride).  Plain reads
+    // were narrowed to the words used -- ds_read_b64 / b96 / read2_b32, whose
+    // lane groups the padded layout does not spread (54.7 M conflict cycles
+    // per launch at 31 taps, float in).
+    typedef float f4v_t __attribute__((ext_vector_type(4)));
+    auto rd = [&](int g) {
+        const f4v_t w = *(const volatile __attribute__((address_space(3))) f4v_t *)(&fl[slot(g)]);
+        return make_float4(w[0], w[1], w[2], w[3]);
+    };
     auto fill = [&](S (&dst)[4], int m) {
         if constexpr (SPG == 4) {
-            const float4 v = fl[slot(gb + m / 4)];
+            const float4 v = rd(gb + m / 4);
             dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
         } else {
-            const float4 v0 = fl[slot(gb + m / 2)], v1 = fl[slot(gb + m / 2 + 1)];
+            const float4 v0 = rd(gb + m / 2), v1 = rd(gb + m / 2 + 1);
             dst[0] = make_float2(v0.x, v0.y); dst[1] = make_float2(v0.z, v0.w);
             dst[2] = make_float2(v1.x, v1.y); dst[3] = make_float2(v1.z, v1.w);
         }
