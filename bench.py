@@ -180,9 +180,11 @@ class DecimWorkload(Workload):
 class MixDecimWorkload(Workload):
     dtype = "i32"
     bytes_per_sample = 5.0  # 4 B complex<int16_t> read + 4 B out per 4 inputs
-    # 127 taps -> 64 int16 tap pairs x 2 components per output, 1 output per 4
-    # inputs: 32 v_dot2 lane-ops per input sample (the mixer's own ~9 ops not counted)
-    dot2_per_sample = 32.0
+    # algorithmic dot2 work per input sample: the decimator's 127 taps x 2
+    # components per output, 1 output per 4 inputs = 63.5 int MACs = 31.75
+    # v_dot2 lane-ops (the kernel issues 32: 64 tap pairs, the last with a zero
+    # tap), plus the mixer's complex product = 4 MACs = 2 v_dot2
+    dot2_per_sample = 33.75
 
     def __init__(self, S, torch, L, channels, rank, fp):
         from srcdsp_amd.design import hamming_sinc, q14
@@ -282,7 +284,7 @@ class Ci16DecimWorkload(Workload):
     127 Q14 taps, no mixer (config 4's decimator)."""
     dtype = "i32"
     bytes_per_sample = 5.0
-    dot2_per_sample = 32.0
+    dot2_per_sample = 31.75  # 127 taps x 2 components / 4 = 63.5 int MACs (the kernel issues 32 dot2)
 
     def __init__(self, S, torch, L, channels, rank, fp):
         from srcdsp_amd.design import hamming_sinc, q14
