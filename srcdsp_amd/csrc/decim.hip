@@ -234,8 +234,18 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
     if (f.M == 1 && (f.kv == KV_CF32 || f.kv == KV_F32_REAL) && al && out_al && f.ntaps <= kFirMaxTaps && !mixed) {
         rc = f.kv == KV_CF32 ? launch_fir_tile<KV_CF32>(L, channels, fma, s)
                              : launch_fir_tile<KV_F32_REAL>(L, channels, fma, s);
-    } else if (f.M == 4 && f.kv == KV_CF32 && al && (f.ntaps == 127 || f.ntaps == 128)) {
-        rc = f.ntaps == 127 ? launch_cf32<127>(L, channels, fma, s) : launch_cf32<128>(L, channels, fma, s);
+    } else if (f.M == 4 && f.kv == KV_CF32 && al &&
+               (f.ntaps == 63 || f.ntaps == 64 || f.ntaps == 127 || f.ntaps == 128 || f.ntaps == 255 || f.ntaps == 256)) {
+        // the headline kernel, compiled per tap count: 127/128 (BASELINE configs 2 and
+        // 3) and the neighbouring power-of-two lengths
+        switch (f.ntaps) {
+        case 63: rc = launch_cf32<63>(L, channels, fma, s); break;
+        case 64: rc = launch_cf32<64>(L, channels, fma, s); break;
+        case 127: rc = launch_cf32<127>(L, channels, fma, s); break;
+        case 128: rc = launch_cf32<128>(L, channels, fma, s); break;
+        case 255: rc = launch_cf32<255>(L, channels, fma, s); break;
+        default: rc = launch_cf32<256>(L, channels, fma, s); break;
+        }
     } else if (f.M == 4 && f.kv == KV_CI16_I32 && f.coef_fits_i16 && al && (f.ntaps == 127 || f.ntaps == 128)) {
         DecimLaunch L2 = L;
         L2.coef = f.d_cpair;

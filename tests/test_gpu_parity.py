@@ -58,13 +58,14 @@ def _chunks(total, sizes):
 
 
 @pytest.mark.parametrize("fp", ["fma", "strict"])
-@pytest.mark.parametrize("ntaps", [127, 128])
+@pytest.mark.parametrize("ntaps", [63, 64, 127, 128, 255, 256])
 def test_decim_cf32_tile_kernel_vs_oracle(S, O, fp, ntaps):
-    """Headline instantiation through the tile kernel: many tiles, tail tiles,
-    history carried over uneven calls (incl. calls shorter than a tile)."""
+    """The headline kernel at every tap count it is compiled for (M = 4): many
+    tiles, tail tiles, history carried over uneven calls (incl. calls shorter
+    than a tile)."""
     from srcdsp_amd.design import hamming_sinc
-    c = hamming_sinc(127)
-    if ntaps == 128:
+    c = hamming_sinc(ntaps - (ntaps % 2 == 0))
+    if ntaps % 2 == 0:  # an even count: a trailing zero tap, as the 128-tap form of the 127-tap filter
         c = np.concatenate([c, [0.0]]).astype(np.float32)
     x = O[fp].gen_cf32(0x5EED, 3, 0, 1 << 20, -32768, 32767)
     x = x + np.float32(0.37)  # non-integer inputs exercise rounding
