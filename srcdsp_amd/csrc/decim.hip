@@ -57,9 +57,13 @@ constexpr int kCfR = 4, kCfBlock = 512, kCfGrid = 1024;
 constexpr int kCfGridCap = 2048;  // persistent grid of the other streaming kernels
 constexpr int kCiR = 4, kCiBlock = 256;
 
-template <int NT>
+// M = 4 is the headline; M = 8 uses the same kernel with R = 2 outputs per
+// lane (the same 16-sample lane chunks, LDS image and memory schedule).  M = 2
+// (R = 8) spills at the 128-VGPR budget of 16 waves per CU and stays on
+// decim_tile.
+template <int NT, int M = 4>
 int launch_cf32(DecimLaunch L, int channels, bool fma, hipStream_t s) {
-    constexpr int TO = kCfBlock * kCfR;
+    constexpr int R = 16 / M, TO = kCfBlock * R;
     L.ntiles = (L.n_out + TO - 1) / TO;
     dim3 grid((unsigned)std::min<long>(L.ntiles, kCfGrid), channels);
     const bool q0 = (L.shift & 31u) == 0;  // limitScale16 shift 0: the 4-op float quantiser
@@ -72,7 +76,7 @@ int launch_cf32(DecimLaunch L, int channels, bool fma, hipStream_t s) {
     // 1.08 M cycles per launch, -8.6 % time on one box,
     // profiles/tuning/r02_ramp_ab.txt)
 #define SRCDSP_CF32(F, Q) \
-    hipLaunchKernelGGL((decim_stream2_cf32<NT, kCfR, kCfBlock, F, 4, Q, 0, true, 2, true, true, -1, -1, true>), grid, \
+    hipLaunchKernelGGL((decim_stream2_cf32<NT, R, kCfBlock, F, 4, Q, 0, true, 2, true, true, -1, -1, true, M>), grid, \
                        dim3(kCfBlock), 0, s, L)
     if (fma && q0)
         SRCDSP_CF32(true, true);
@@ -245,6 +249,13 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
         case 128: rc = launch_cf32<128>(L, channels, fma, s); break;
         case 255: rc = launch_cf32<255>(L, channels, fma, s); break;
         default: rc = launch_cf32<256>(L, channels, fma, s); break;
+        }
+    } else if (f.M == 8 && f.kv == KV_CF32 && al && (f.ntaps == 127 || f.ntaps == 128 || f.ntaps == 255 || f.ntaps == 256)) {
+        switch (f.ntaps) {
+        case 127: rc = launch_cf32<127, 8>(L, channels, fma, s); break;
+        case 128: rc = launch_cf32<128, 8>(L, channels, fma, s); break;
+        case 255: rc = launch_cf32<255, 8>(L, channels, fma, s); break;
+        default: rc = launch_cf32<256, 8>(L, channels, fma, s); break;
         }
     } else if (f.M == 4 && f.kv == KV_CI16_I32 && f.coef_fits_i16 && al && (f.ntaps == 127 || f.ntaps == 128)) {
         DecimLaunch L2 = L;

@@ -186,7 +186,8 @@ __device__ __forceinline__ float q16f_shift0(float y) {
     return __builtin_fabsf(y) < 2147483648.0f ? t : 0.0f;
 }
 
-// Persistent complex<float> decimator, M = 4 (the headline, a1).
+// Persistent complex<float> decimator, M = 4 (the headline, a1), and M = 8
+// with the same 16-sample lane chunks (R = 16/M outputs per lane).
 // A tile is BLOCK*R outputs; its input span (4*BLOCK*R samples + a 4*NQ
 // sample halo, NQ = ceil(NT/4)) is staged HBM -> VGPR -> LDS as 16-B granules
 // (2 samples).  LDS granule of tile granule g:
@@ -274,17 +275,18 @@ __device__ __forceinline__ void store_wave_lines(float2 *wo, const float2 (&o)[R
 // second pair with lane i's, so each of the two store instructions writes
 // 1 KiB of whole lines, with no LDS round trip and no barrier.
 template <int NT, int R, int BLOCK, bool FMA, int MINW, bool Q0, int PROBE = 0, bool NTL = false, int OST = 0,
-          bool NTS = false, bool GS = false, int LAUX = -1, int SAUX = -1, bool ILV = false>
+          bool NTS = false, bool GS = false, int LAUX = -1, int SAUX = -1, bool ILV = false, int M = 4>
 __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a) {
-    static_assert(OST != 2 || R == 4 || R == 8, "whole-line stores assume 4 or 8 outputs per lane");
+    static_assert(OST != 2 || R == 2 || R == 4 || R == 8, "whole-line stores assume 2, 4 or 8 outputs per lane");
+    static_assert(M * R == 16 && (M == 4 || ILV), "a lane chunk is 16 input samples; M != 4 takes the ILV tap loop");
 #ifndef SRCDSP_TUNING
     // the probe / cache-policy / issue-order variants exist for scripts/tune only
     static_assert(PROBE == 0 && LAUX < 0 && SAUX < 0, "tuning-only variant: build with -DSRCDSP_TUNING");
 #endif
     constexpr int NQ = (NT + 3) / 4;
     constexpr int TO = BLOCK * R;
-    constexpr int TG = 2 * TO + 2 * NQ;
-    constexpr int PR = 2 * R;
+    constexpr int TG = M * TO / 2 + 2 * NQ;  // staged granules: M TO input samples + the halo
+    constexpr int PR = M * R / 2;  // granules per lane chunk (16 samples)
     constexpr int KPAD = ceildiv(2 * NQ, PR);
     constexpr int LG = TG + (TG + KPAD * PR) / PR + 1;
     constexpr int PER = ceildiv(TG, BLOCK);
@@ -312,7 +314,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
     // tiles >= 1: one descriptor per tile, 32-bit lane offsets, range-checked
     auto stage_load = [&](float4 (&v)[PER], long tile) {
         if constexpr (PROBE >= 2) tile = 1 + (tile & 15);
-        const long b0 = 4 * tile * TO - 4 * NQ;  // >= 0 for tile >= 1
+        const long b0 = M * tile * TO - 4 * NQ;  // >= 0 for tile >= 1
         const long remb = (n_in - b0) * 8;
         const unsigned nrec = (unsigned)(remb > 0xfffffff0L ? 0xfffffff0L : (remb < 0 ? 0 : remb));
         __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)(in + b0), 0, nrec, 0x00020000);
@@ -367,7 +369,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
         constexpr bool WHOLE = decltype(whole_tag)::value;
         ConstPtr<float> tp = const_view<float>(a.coef);
         asm volatile("" : "+s"(tp));
-        float2 X[4 * (NQ + R)];
+        constexpr int GPC = M * R / 4;  // 4-sample groups per lane chunk
+        float2 X[4 * (NQ + GPC)];
         float yr[R], yi[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) yr[r] = yi[r] = 0.f;
@@ -380,10 +383,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
             X[4 * e + 4 * NQ + 3] = make_float2(g1.z, g1.w);
         };
 #pragma unroll
-        for (int e = -1; e < R; ++e) load_group(e);
+        for (int e = -1; e < GPC; ++e) load_group(e);
         if constexpr (PROBE == 1 || PROBE == 3) {
 #pragma unroll
-            for (int r = 0; r < R; ++r) { yr[r] = X[4 * r + 4 * NQ].x; yi[r] = X[4 * r + 4 * NQ].y; }
+            for (int r = 0; r < R; ++r) { yr[r] = X[M * r + 4 * NQ].x; yi[r] = X[M * r + 4 * NQ].y; }
         } else if constexpr (ILV && PROBE != 3) {
             // tap-major issue order through inline asm: R independent chains
             // round-robin, taps as SGPR pairs (c[2m], c[2m+1]); FMA: one
@@ -407,7 +410,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
                         if constexpr (FMA) {
 #pragma unroll
                             for (int r = 0; r < R; ++r) {
-                                const float2 x = X[4 * (r - q) - p + 4 * NQ];
+                                const float2 x = X[M * r - 4 * q - p + 4 * NQ];
                                 const f2_t xv = {x.x, x.y};
                                 if (k == 0) pk_fma_tap<false, true>(acc[r], cp, xv);
                                 else if (k & 1) pk_fma_tap<true, false>(acc[r], cp, xv);
@@ -417,7 +420,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
                             f2_t pr[R];
 #pragma unroll
                             for (int r = 0; r < R; ++r) {
-                                const float2 x = X[4 * (r - q) - p + 4 * NQ];
+                                const float2 x = X[M * r - 4 * q - p + 4 * NQ];
                                 const f2_t xv = {x.x, x.y};
                                 if (k & 1) pk_mul_tap<true>(pr[r], cp, xv);
                                 else pk_mul_tap<false>(pr[r], cp, xv);
@@ -454,6 +457,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
         const unsigned sh = a.shift;
         auto q = [&](float y) { return Q0 ? q16f_shift0(y) : q16f(y, sh); };
         if (PROBE == 5 && a.ntaps != 12345) {  // tuning: no stores
+        } else if constexpr (OST == 2 && WHOLE && R == 2) {  // 16 B per lane: whole lines as they stand
+            store16<NTS>((float4 *)(out + n0), make_float4(q(yr[0]), q(yi[0]), q(yr[1]), q(yi[1])));
         } else if constexpr (OST == 2 && WHOLE) {
             float2 o[R];
 #pragma unroll

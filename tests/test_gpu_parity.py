@@ -58,9 +58,10 @@ def _chunks(total, sizes):
 
 
 @pytest.mark.parametrize("fp", ["fma", "strict"])
-@pytest.mark.parametrize("ntaps", [63, 64, 127, 128, 255, 256])
-def test_decim_cf32_tile_kernel_vs_oracle(S, O, fp, ntaps):
-    """The headline kernel at every tap count it is compiled for (M = 4): many
+@pytest.mark.parametrize("M,ntaps", [(4, 63), (4, 64), (4, 127), (4, 128), (4, 255), (4, 256),
+                                     (8, 127), (8, 128), (8, 255), (8, 256)])
+def test_decim_cf32_tile_kernel_vs_oracle(S, O, fp, M, ntaps):
+    """The headline kernel at every (M, tap count) it is compiled for: many
     tiles, tail tiles, history carried over uneven calls (incl. calls shorter
     than a tile)."""
     from srcdsp_amd.design import hamming_sinc
@@ -69,10 +70,10 @@ def test_decim_cf32_tile_kernel_vs_oracle(S, O, fp, ntaps):
         c = np.concatenate([c, [0.0]]).astype(np.float32)
     x = O[fp].gen_cf32(0x5EED, 3, 0, 1 << 20, -32768, 32767)
     x = x + np.float32(0.37)  # non-integer inputs exercise rounding
-    ref = O[fp].decim(0, 4, c)
-    g = S.FilterDnsamplingFir(c, 4, fp=fp)
-    for off, n in _chunks(len(x), [400000, 8, 2048 * 4 + 4, 131072, 128, 300004]):
-        n -= n % 4
+    ref = O[fp].decim(0, M, c)
+    g = S.FilterDnsamplingFir(c, M, fp=fp)
+    for off, n in _chunks(len(x), [400000, 8, 2048 * M + M, 131072, 128, 300004]):
+        n -= n % M
         if n == 0:
             continue
         xs = x[off:off + n]
