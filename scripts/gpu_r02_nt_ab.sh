@@ -13,4 +13,4 @@ for round in 1 2; do
     SRCDSP_HIP_LIB=$PWD/$lib timeout -k 10 200 python3 -u scripts/shape_envelope.py >> gpurun_out/nt_ab.txt 2>&1 || exit $?
   done
 done
-grep -E "^##|M=4|M=8" gpurun_out/nt_ab.txt
+grep -E "^##|M=2|M=4|M=8" gpurun_out/nt_ab.txt

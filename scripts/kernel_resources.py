@@ -29,5 +29,5 @@ except OSError:
     dem = [r["name"] for r in rows]
 for r, d in zip(rows, dem):
     if filt in d:
-        print(f"{d[:90]:90s} VGPR {r.get('VGPRs','?'):>4s} AGPR {r.get('AGPRs','?'):>3s} "
+        print(f"{d[:int(sys.argv[3]) if len(sys.argv) > 3 else 90]:90s} VGPR {r.get('VGPRs','?'):>4s} AGPR {r.get('AGPRs','?'):>3s} "
               f"scratch {r.get('ScratchSize [bytes/lane]','?'):>4s} occ {r.get('Occupancy [waves/SIMD]','?')}")

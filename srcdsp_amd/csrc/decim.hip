@@ -58,12 +58,12 @@ constexpr int kCfGridCap = 2048;  // persistent grid of the other streaming kern
 constexpr int kCiR = 4, kCiBlock = 256;
 
 // M = 4 is the headline; M = 8 uses the same kernel with R = 2 outputs per
-// lane (the same 16-sample lane chunks, LDS image and memory schedule).  M = 2
-// (R = 8) spills at the 128-VGPR budget of 16 waves per CU and stays on
-// decim_tile.
+// lane (the same 16-sample lane chunks, LDS image and memory schedule), M = 2
+// with R = 4 (8-sample lane chunks: R = 8 spills at the 128-VGPR budget of 16
+// waves per CU).
 template <int NT, int M = 4>
 int launch_cf32(DecimLaunch L, int channels, bool fma, hipStream_t s) {
-    constexpr int R = 16 / M, TO = kCfBlock * R;
+    constexpr int R = M == 2 ? 4 : 16 / M, TO = kCfBlock * R;
     L.ntiles = (L.n_out + TO - 1) / TO;
     dim3 grid((unsigned)std::min<long>(L.ntiles, kCfGrid), channels);
     const bool q0 = (L.shift & 31u) == 0;  // limitScale16 shift 0: the 4-op float quantiser
@@ -249,6 +249,13 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
         case 128: rc = launch_cf32<128>(L, channels, fma, s); break;
         case 255: rc = launch_cf32<255>(L, channels, fma, s); break;
         default: rc = launch_cf32<256>(L, channels, fma, s); break;
+        }
+    } else if (f.M == 2 && f.kv == KV_CF32 && al && (f.ntaps == 63 || f.ntaps == 64 || f.ntaps == 127 || f.ntaps == 128)) {
+        switch (f.ntaps) {
+        case 63: rc = launch_cf32<63, 2>(L, channels, fma, s); break;
+        case 64: rc = launch_cf32<64, 2>(L, channels, fma, s); break;
+        case 127: rc = launch_cf32<127, 2>(L, channels, fma, s); break;
+        default: rc = launch_cf32<128, 2>(L, channels, fma, s); break;
         }
     } else if (f.M == 8 && f.kv == KV_CF32 && al && (f.ntaps == 127 || f.ntaps == 128 || f.ntaps == 255 || f.ntaps == 256)) {
         switch (f.ntaps) {

@@ -186,8 +186,8 @@ __device__ __forceinline__ float q16f_shift0(float y) {
     return __builtin_fabsf(y) < 2147483648.0f ? t : 0.0f;
 }
 
-// Persistent complex<float> decimator, M = 4 (the headline, a1), and M = 8
-// with the same 16-sample lane chunks (R = 16/M outputs per lane).
+// Persistent complex<float> decimator, M = 4 (the headline, a1), and M = 8 / 2
+// with R = 2 / 4 outputs per lane (lane chunks of M R = 16 / 8 input samples).
 // A tile is BLOCK*R outputs; its input span (4*BLOCK*R samples + a 4*NQ
 // sample halo, NQ = ceil(NT/4)) is staged HBM -> VGPR -> LDS as 16-B granules
 // (2 samples).  LDS granule of tile granule g:
@@ -278,7 +278,8 @@ template <int NT, int R, int BLOCK, bool FMA, int MINW, bool Q0, int PROBE = 0, 
           bool NTS = false, bool GS = false, int LAUX = -1, int SAUX = -1, bool ILV = false, int M = 4>
 __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a) {
     static_assert(OST != 2 || R == 2 || R == 4 || R == 8, "whole-line stores assume 2, 4 or 8 outputs per lane");
-    static_assert(M * R == 16 && (M == 4 || ILV), "a lane chunk is 16 input samples; M != 4 takes the ILV tap loop");
+    static_assert((M * R) % 4 == 0 && M * R <= 16 && (M == 4 || ILV),
+                  "a lane chunk is 4, 8, 12 or 16 input samples; M != 4 takes the ILV tap loop");
 #ifndef SRCDSP_TUNING
     // the probe / cache-policy / issue-order variants exist for scripts/tune only
     static_assert(PROBE == 0 && LAUX < 0 && SAUX < 0, "tuning-only variant: build with -DSRCDSP_TUNING");
@@ -286,7 +287,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
     constexpr int NQ = (NT + 3) / 4;
     constexpr int TO = BLOCK * R;
     constexpr int TG = M * TO / 2 + 2 * NQ;  // staged granules: M TO input samples + the halo
-    constexpr int PR = M * R / 2;  // granules per lane chunk (16 samples)
+    constexpr int PR = M * R / 2;  // granules per lane chunk (M R samples)
     constexpr int KPAD = ceildiv(2 * NQ, PR);
     constexpr int LG = TG + (TG + KPAD * PR) / PR + 1;
     constexpr int PER = ceildiv(TG, BLOCK);
