@@ -268,6 +268,17 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
         DecimLaunch L2 = L;
         L2.coef = f.d_cpair;
         rc = f.ntaps == 127 ? launch_ci16_dot2<127>(L2, channels, mixed, s) : launch_ci16_dot2<128>(L2, channels, mixed, s);
+    } else if (f.M == 4 && f.kv == KV_CI16_I32 && f.coef_fits_i16 && al && !mixed &&
+               (f.ntaps == 63 || f.ntaps == 64 || f.ntaps == 255 || f.ntaps == 256)) {
+        // the dot2 kernel's product shape at the neighbouring power-of-two lengths
+        DecimLaunch L2 = L;
+        L2.coef = f.d_cpair;
+        switch (f.ntaps) {
+        case 63: rc = launch_ci16_dot2_shape<63, 512, 0>(L2, channels, false, s); break;
+        case 64: rc = launch_ci16_dot2_shape<64, 512, 0>(L2, channels, false, s); break;
+        case 255: rc = launch_ci16_dot2_shape<255, 512, 0>(L2, channels, false, s); break;
+        default: rc = launch_ci16_dot2_shape<256, 512, 0>(L2, channels, false, s); break;
+        }
     } else if (f.M == 4 && f.kv == KV_CI16_I32 && f.coef_fits_i24 && al && (f.ntaps == 127 || f.ntaps == 128)) {
         rc = f.ntaps == 127 ? launch_ci16<127>(L, channels, mixed, s) : launch_ci16<128>(L, channels, mixed, s);
     } else if ((f.kv == KV_CF32 || f.kv == KV_CI16_I32 || f.kv == KV_CI16_I16) &&

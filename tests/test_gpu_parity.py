@@ -158,6 +158,23 @@ def test_decim_tile_large_calls_vs_oracle(S, O, kind, M, ntaps):
         assert np.array_equal(g.step(dev(xs)).cpu().numpy(), r.step(xs)), (off, n)
 
 
+@pytest.mark.parametrize("ntaps", [63, 64, 127, 128, 255, 256])
+def test_decim_ci16_dot2_tap_counts_vs_oracle(S, O, ntaps):
+    """The v_dot2 decimator (int16-range taps, M = 4) at every tap count it is
+    compiled for: full-scale inputs (accumulator wrap, output saturation), many
+    tiles, a tail tile, history carried over uneven calls."""
+    rng = np.random.default_rng(1000 + ntaps)
+    c = rng.integers(-32768, 32768, size=ntaps).astype(np.int32)
+    c[0], c[-1] = 32767, -32768
+    x = O["strict"].gen_ci16(77 + ntaps, 4, 0, 1 << 20, -32768, 32767)
+    g = S.FilterDnsamplingFir(c, 4, "complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int32_t")
+    r = O["strict"].decim(1, 4, c)
+    for off, n in _chunks(len(x), [400000, 8, 2048 * 4 + 4, 131072, 128, 300004]):
+        n -= n % 4
+        xs = x[off:off + n]
+        assert np.array_equal(g.step(dev(xs)).cpu().numpy(), r.step(xs)), (off, n)
+
+
 @pytest.mark.parametrize("kind", ["i16", "i24", "i32"])
 @pytest.mark.parametrize("ntaps", [1, 16, 17, 31, 100, 1024])
 def test_fir_ci16_tile_vs_oracle(S, O, kind, ntaps):
