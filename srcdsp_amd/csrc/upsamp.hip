@@ -518,14 +518,21 @@ static int up_launch(srcdsp_up_state &u, const void *d_in, size_t n_in, void *d_
 #define SRCDSP_UP_DOT2(LR)                                                                                        \
     hipLaunchKernelGGL((up_tile_dot2<LR, true, WSV, MW, PPV>), grid, dim3(kUpBlockD), smem, s, (const uint32_t *)d_in, (long)n_in, \
                        n_total, (const uint32_t *)hin0, (uint32_t *)hout0, u.d_pair, u.H, shift, (uint32_t *)d_out)
-        // 32 taps per phase (L = 4 x 128 taps, L = 2 x 64): a compile-time shape
-        if (u.L == 2 && PP == 16) {
-            constexpr int WSV = 3, MW = 1, PPV = 16;
-            SRCDSP_UP_DOT2(2);
-        } else if (u.L == 4 && PP == 16) {
-            constexpr int WSV = 3, MW = 1, PPV = 16;
-            SRCDSP_UP_DOT2(4);
-        } else if (u.L == 2) {
+        // 16, 32 or 64 taps per phase (L = 4 x 64 / 128 / 256 taps, L = 2 x 32 /
+        // 64 / 128): compile-time shapes
+#define SRCDSP_UP_PP(LR, P)                              \
+    if (u.L == LR && PP == P) {                          \
+        constexpr int WSV = 3, MW = 1, PPV = P;          \
+        SRCDSP_UP_DOT2(LR);                              \
+    } else
+        SRCDSP_UP_PP(2, 8)
+        SRCDSP_UP_PP(2, 16)
+        SRCDSP_UP_PP(2, 32)
+        SRCDSP_UP_PP(4, 8)
+        SRCDSP_UP_PP(4, 16)
+        SRCDSP_UP_PP(4, 32)
+#undef SRCDSP_UP_PP
+        if (u.L == 2) {
             constexpr int WSV = 3, MW = 1, PPV = 0;
             SRCDSP_UP_DOT2(2);
         } else {
