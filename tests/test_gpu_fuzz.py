@@ -2,8 +2,9 @@
 tests/test_oracle_golden.py pins to the reference): random operator shapes,
 random chains of step() calls of ragged lengths (including 0 and 1), resets,
 left shifts and coefficient changes, device-resident and host-staged calls
-interleaved.  Every output byte must match.  Shapes are drawn to hit the tile
-kernels (127/128 taps, M = 4, M = 1, L = 2/4) as often as the generic ones."""
+interleaved.  Every output byte must match.  Shapes are drawn to hit the tuned
+kernels (63/64/127/128/255/256 taps at M = 2/4/8, M = 1, L = 2/4 with 16/32/64
+taps per phase) as often as the generic ones."""
 import numpy as np
 import pytest
 
@@ -60,12 +61,12 @@ def _input(rng, O, variant, n):
     return O["fma"].gen_ci16(int(rng.integers(1 << 30)), 0, 0, n, -32768, 32767)
 
 
-@pytest.mark.parametrize("seed", range(24))
+@pytest.mark.parametrize("seed", range(40))
 def test_fuzz_decimator(S, O, seed):
     rng = np.random.default_rng(1000 + seed)
     variant = int(rng.integers(0, 4))
     M = int(rng.choice([1, 2, 3, 4, 4, 4, 5, 8]))
-    ntaps = int(rng.choice([1, 2, 7, 31, 63, 127, 127, 128, 129, 200]))
+    ntaps = int(rng.choice([1, 2, 7, 31, 63, 64, 127, 127, 128, 129, 200, 255, 256]))
     fp = str(rng.choice(["fma", "strict"]))
     c = _taps(rng, variant, ntaps)
     g = S.FilterDnsamplingFir(c, M, *_DECIM_T[variant], fp=fp)
@@ -80,7 +81,7 @@ def test_fuzz_decimator(S, O, seed):
             g.setLeftShiftBy2(ls)
             r.set_left_shift(ls)
         elif u < 0.2:
-            c = _taps(rng, variant, int(rng.choice([ntaps, 1, 64, 127, 128])))
+            c = _taps(rng, variant, int(rng.choice([ntaps, 1, 63, 64, 127, 128, 255])))
             g.setCoeffs(c, require_multiple=False)
             r.set_coeffs(c)
         n = M * int(rng.choice([0, 1, 3, 17, 1024, 4099, 20000, int(rng.integers(0, 30000))]))
@@ -117,7 +118,7 @@ def test_fuzz_upsampler(S, O, seed):
     rng = np.random.default_rng(3000 + seed)
     variant = int(rng.integers(0, 3))
     L = int(rng.choice([1, 2, 3, 4, 4, 8]))
-    H = int(rng.choice([1, 2, 5, 32, 33, 70]))
+    H = int(rng.choice([1, 2, 5, 16, 32, 33, 64, 70]))
     lim = {0: int(rng.choice([32767, 1 << 22, 1 << 26])), 1: 32767, 2: 30000}[variant]
     c = rng.integers(-lim, lim + 1, L * H)
     g = S.FilterUpsamplingFir(c, L, *_UP_T[variant])
