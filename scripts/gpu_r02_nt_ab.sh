@@ -4,7 +4,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 500 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fuzz.py -x -q --timeout 240 --timeout-method thread \
-  -k "decim or golden or fuzz" > gpurun_out/nt_tests.log 2>&1 || { tail -30 gpurun_out/nt_tests.log; exit 1; }
+  -k "decim or golden or fuzz or fir" > gpurun_out/nt_tests.log 2>&1 || { tail -30 gpurun_out/nt_tests.log; exit 1; }
 tail -2 gpurun_out/nt_tests.log
 : > gpurun_out/nt_ab.txt
 for round in 1 2; do
@@ -13,4 +13,4 @@ for round in 1 2; do
     SRCDSP_HIP_LIB=$PWD/$lib timeout -k 10 200 python3 -u scripts/shape_envelope.py >> gpurun_out/nt_ab.txt 2>&1 || exit $?
   done
 done
-grep -E "^##|M=2|M=4|M=8" gpurun_out/nt_ab.txt
+grep -E "^##|M=" gpurun_out/nt_ab.txt

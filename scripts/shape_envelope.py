@@ -11,7 +11,7 @@ from srcdsp_amd.design import hamming_sinc
 L = 1 << 26
 x = torch.empty(L, dtype=torch.complex64, device="cuda")
 S.fill_synthetic(x, "cf32", seed=0x5EED, channel=0)
-for M, N in ((4, 127), (4, 128), (4, 63), (4, 255), (2, 63), (2, 127), (8, 127), (8, 255), (1, 31), (1, 127), (1, 255)):
+for M, N in ((4, 127), (4, 128), (4, 63), (4, 255), (2, 63), (2, 127), (8, 127), (8, 255), (1, 31), (1, 63), (1, 127), (1, 255)):
     f = S.FilterDnsamplingFir(hamming_sinc(N), M, fp="fma") if M > 1 else S.FilterFir(hamming_sinc(N), fp="fma")
     y = torch.empty(L // M, dtype=torch.complex64, device="cuda")
     for _ in range(10):

@@ -59,11 +59,11 @@ constexpr int kCiR = 4, kCiBlock = 256;
 
 // M = 4 is the headline; M = 8 uses the same kernel with R = 2 outputs per
 // lane (the same 16-sample lane chunks, LDS image and memory schedule), M = 2
-// with R = 4 (8-sample lane chunks: R = 8 spills at the 128-VGPR budget of 16
-// waves per CU).
+// with R = 4 and M = 1 (complex<float> FilterFir) with R = 8, both on 8-sample
+// lane chunks (R = 8 at M = 2 spills at the 128-VGPR budget of 16 waves per CU).
 template <int NT, int M = 4>
 int launch_cf32(DecimLaunch L, int channels, bool fma, hipStream_t s) {
-    constexpr int R = M == 2 ? 4 : 16 / M, TO = kCfBlock * R;
+    constexpr int R = M == 1 ? 8 : (M == 2 ? 4 : 16 / M), TO = kCfBlock * R;
     L.ntiles = (L.n_out + TO - 1) / TO;
     dim3 grid((unsigned)std::min<long>(L.ntiles, kCfGrid), channels);
     const bool q0 = (L.shift & 31u) == 0;  // limitScale16 shift 0: the 4-op float quantiser
@@ -235,7 +235,18 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
     bool al = aligned16(L.in) && ((L.in_stride * kv_in_bytes(f.kv)) % 16 == 0);
     int rc = SRCDSP_OK;
     const bool out_al = aligned16(L.out) && ((L.out_stride * kv_out_bytes(f.kv)) % 16 == 0);
-    if (f.M == 1 && (f.kv == KV_CF32 || f.kv == KV_F32_REAL) && al && out_al && f.ntaps <= kFirMaxTaps && !mixed) {
+    if (f.M == 1 && f.kv == KV_CF32 && al && out_al && !mixed &&
+        (f.ntaps == 63 || f.ntaps == 64 || f.ntaps == 127 || f.ntaps == 128)) {
+        // complex<float> single-rate FIR at the common lengths: the headline kernel
+        // with 8 outputs per lane on 8-sample lane chunks (at 255/256 taps its
+        // register window goes to scratch; those stay on fir_tile_f32)
+        switch (f.ntaps) {
+        case 63: rc = launch_cf32<63, 1>(L, channels, fma, s); break;
+        case 64: rc = launch_cf32<64, 1>(L, channels, fma, s); break;
+        case 127: rc = launch_cf32<127, 1>(L, channels, fma, s); break;
+        default: rc = launch_cf32<128, 1>(L, channels, fma, s); break;
+        }
+    } else if (f.M == 1 && (f.kv == KV_CF32 || f.kv == KV_F32_REAL) && al && out_al && f.ntaps <= kFirMaxTaps && !mixed) {
         rc = f.kv == KV_CF32 ? launch_fir_tile<KV_CF32>(L, channels, fma, s)
                              : launch_fir_tile<KV_F32_REAL>(L, channels, fma, s);
     } else if (f.M == 4 && f.kv == KV_CF32 && al &&

@@ -187,7 +187,8 @@ __device__ __forceinline__ float q16f_shift0(float y) {
 }
 
 // Persistent complex<float> decimator, M = 4 (the headline, a1), and M = 8 / 2
-// with R = 2 / 4 outputs per lane (lane chunks of M R = 16 / 8 input samples).
+// / 1 with R = 2 / 4 / 8 outputs per lane (lane chunks of M R = 16 / 8 / 8
+// input samples; M = 1 is the complex<float> FilterFir).
 // A tile is BLOCK*R outputs; its input span (4*BLOCK*R samples + a 4*NQ
 // sample halo, NQ = ceil(NT/4)) is staged HBM -> VGPR -> LDS as 16-B granules
 // (2 samples).  LDS granule of tile granule g:
