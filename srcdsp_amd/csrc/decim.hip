@@ -63,7 +63,7 @@ constexpr int kCiR = 4, kCiBlock = 256;
 // lane chunks (R = 8 at M = 2 spills at the 128-VGPR budget of 16 waves per CU).
 template <int NT, int M = 4>
 int launch_cf32(DecimLaunch L, int channels, bool fma, hipStream_t s) {
-    constexpr int R = M == 1 ? 8 : (M == 2 ? 4 : 16 / M), TO = kCfBlock * R;
+    constexpr int R = M == 1 ? 8 : (M <= 3 ? 4 : 16 / M), TO = kCfBlock * R;
     L.ntiles = (L.n_out + TO - 1) / TO;
     dim3 grid((unsigned)std::min<long>(L.ntiles, kCfGrid), channels);
     const bool q0 = (L.shift & 31u) == 0;  // limitScale16 shift 0: the 4-op float quantiser
@@ -267,6 +267,20 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
         case 64: rc = launch_cf32<64, 2>(L, channels, fma, s); break;
         case 127: rc = launch_cf32<127, 2>(L, channels, fma, s); break;
         default: rc = launch_cf32<128, 2>(L, channels, fma, s); break;
+        }
+    } else if (f.M == 3 && f.kv == KV_CF32 && al && (f.ntaps == 63 || f.ntaps == 64 || f.ntaps == 127 || f.ntaps == 128)) {
+        switch (f.ntaps) {
+        case 63: rc = launch_cf32<63, 3>(L, channels, fma, s); break;
+        case 64: rc = launch_cf32<64, 3>(L, channels, fma, s); break;
+        case 127: rc = launch_cf32<127, 3>(L, channels, fma, s); break;
+        default: rc = launch_cf32<128, 3>(L, channels, fma, s); break;
+        }
+    } else if (f.M == 16 && f.kv == KV_CF32 && al && (f.ntaps == 127 || f.ntaps == 128 || f.ntaps == 255 || f.ntaps == 256)) {
+        switch (f.ntaps) {
+        case 127: rc = launch_cf32<127, 16>(L, channels, fma, s); break;
+        case 128: rc = launch_cf32<128, 16>(L, channels, fma, s); break;
+        case 255: rc = launch_cf32<255, 16>(L, channels, fma, s); break;
+        default: rc = launch_cf32<256, 16>(L, channels, fma, s); break;
         }
     } else if (f.M == 8 && f.kv == KV_CF32 && al && (f.ntaps == 127 || f.ntaps == 128 || f.ntaps == 255 || f.ntaps == 256)) {
         switch (f.ntaps) {

@@ -186,9 +186,9 @@ __device__ __forceinline__ float q16f_shift0(float y) {
     return __builtin_fabsf(y) < 2147483648.0f ? t : 0.0f;
 }
 
-// Persistent complex<float> decimator, M = 4 (the headline, a1), and M = 8 / 2
-// / 1 with R = 2 / 4 / 8 outputs per lane (lane chunks of M R = 16 / 8 / 8
-// input samples; M = 1 is the complex<float> FilterFir).
+// Persistent complex<float> decimator, M = 4 (the headline, a1), and M = 16 / 8
+// / 3 / 2 / 1 with R = 1 / 2 / 4 / 4 / 8 outputs per lane (lane chunks of M R =
+// 16 / 16 / 12 / 8 / 8 input samples; M = 1 is the complex<float> FilterFir).
 // A tile is BLOCK*R outputs; its input span (4*BLOCK*R samples + a 4*NQ
 // sample halo, NQ = ceil(NT/4)) is staged HBM -> VGPR -> LDS as 16-B granules
 // (2 samples).  LDS granule of tile granule g:
@@ -278,7 +278,7 @@ __device__ __forceinline__ void store_wave_lines(float2 *wo, const float2 (&o)[R
 template <int NT, int R, int BLOCK, bool FMA, int MINW, bool Q0, int PROBE = 0, bool NTL = false, int OST = 0,
           bool NTS = false, bool GS = false, int LAUX = -1, int SAUX = -1, bool ILV = false, int M = 4>
 __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a) {
-    static_assert(OST != 2 || R == 2 || R == 4 || R == 8, "whole-line stores assume 2, 4 or 8 outputs per lane");
+    static_assert(OST != 2 || R == 1 || R == 2 || R == 4 || R == 8, "whole-line stores assume 1, 2, 4 or 8 outputs per lane");
     static_assert((M * R) % 4 == 0 && M * R <= 16 && (M == 4 || ILV),
                   "a lane chunk is 4, 8, 12 or 16 input samples; M != 4 takes the ILV tap loop");
 #ifndef SRCDSP_TUNING
@@ -461,6 +461,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
         if (PROBE == 5 && a.ntaps != 12345) {  // tuning: no stores
         } else if constexpr (OST == 2 && WHOLE && R == 2) {  // 16 B per lane: whole lines as they stand
             store16<NTS>((float4 *)(out + n0), make_float4(q(yr[0]), q(yi[0]), q(yr[1]), q(yi[1])));
+        } else if constexpr (OST == 2 && WHOLE && R == 1) {  // 8 B per lane, lane-contiguous
+            out[n0] = make_float2(q(yr[0]), q(yi[0]));
         } else if constexpr (OST == 2 && WHOLE) {
             float2 o[R];
 #pragma unroll

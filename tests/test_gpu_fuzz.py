@@ -3,7 +3,7 @@ tests/test_oracle_golden.py pins to the reference): random operator shapes,
 random chains of step() calls of ragged lengths (including 0 and 1), resets,
 left shifts and coefficient changes, device-resident and host-staged calls
 interleaved.  Every output byte must match.  Shapes are drawn to hit the tuned
-kernels (63/64/127/128/255/256 taps at M = 2/4/8, M = 1, L = 2/4 with 16/32/64
+kernels (63/64/127/128/255/256 taps at M = 1/2/3/4/8/16, M = 1, L = 2/4 with 16/32/64
 taps per phase) as often as the generic ones."""
 import numpy as np
 import pytest
@@ -65,7 +65,7 @@ def _input(rng, O, variant, n):
 def test_fuzz_decimator(S, O, seed):
     rng = np.random.default_rng(1000 + seed)
     variant = int(rng.integers(0, 4))
-    M = int(rng.choice([1, 2, 3, 4, 4, 4, 5, 8]))
+    M = int(rng.choice([1, 2, 3, 4, 4, 4, 5, 8, 16]))
     ntaps = int(rng.choice([1, 2, 7, 31, 63, 64, 127, 127, 128, 129, 200, 255, 256]))
     fp = str(rng.choice(["fma", "strict"]))
     c = _taps(rng, variant, ntaps)

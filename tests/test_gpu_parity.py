@@ -60,7 +60,8 @@ def _chunks(total, sizes):
 @pytest.mark.parametrize("fp", ["fma", "strict"])
 @pytest.mark.parametrize("M,ntaps", [(4, 63), (4, 64), (4, 127), (4, 128), (4, 255), (4, 256),
                                      (8, 127), (8, 128), (8, 255), (8, 256), (2, 63), (2, 64), (2, 127), (2, 128),
-                                     (1, 63), (1, 64), (1, 127), (1, 128)])
+                                     (1, 63), (1, 64), (1, 127), (1, 128), (3, 63), (3, 64), (3, 127), (3, 128),
+                                     (16, 127), (16, 128), (16, 255), (16, 256)])
 def test_decim_cf32_tile_kernel_vs_oracle(S, O, fp, M, ntaps):
     """The headline kernel at every (M, tap count) it is compiled for: many
     tiles, tail tiles, history carried over uneven calls (incl. calls shorter
