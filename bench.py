@@ -104,8 +104,11 @@ def dry_run(args) -> None:
         dist.all_reduce(t)
         seen = int(t.item())
         dist.destroy_process_group()
-    print(json.dumps({"dry_run": True, "rank": rank, "world": world, "world_seen": seen, "gpus": args.gpus}),
-          flush=True)
+    # one write() per line: the ranks share the launcher's stdout pipe, and a
+    # print() (text, then newline) from two ranks can interleave on one line
+    sys.stdout.flush()
+    os.write(1, (json.dumps({"dry_run": True, "rank": rank, "world": world, "world_seen": seen,
+                             "gpus": args.gpus}) + "\n").encode())
     if world != args.gpus or seen != args.gpus:
         raise SystemExit(f"bench: rank {rank} sees world {world}/{seen}, --gpus {args.gpus}")
 
