@@ -107,17 +107,15 @@ int launch_ci16(DecimLaunch L, int channels, bool mixed, hipStream_t s) {
 // tuning build (-DSRCDSP_TUNING, scripts/tune) can pick another with
 // SRCDSP_CI16_VARIANT = 0: 256 lanes, 1: 512 lanes, 2: 256 lanes + doubled
 // table, 3: 512 lanes + doubled table, 4 (product): 512 lanes + sequence table.
-static int ci16_variant() {
 #ifdef SRCDSP_TUNING
+static int ci16_variant() {
     static const int v = [] {
         const char *e = std::getenv("SRCDSP_CI16_VARIANT");
         return e ? std::atoi(e) : 4;
     }();
     return v;
-#else
-    return 4;
-#endif
 }
+#endif
 
 // period of the fused mixer's table index over input samples, extended to a
 // multiple of 4 (one 16-B table read per staged granule): lcm(N / gcd(freq, N), 4)
@@ -149,18 +147,22 @@ int launch_ci16_dot2_shape(DecimLaunch L, int channels, bool mixed, hipStream_t 
 
 template <int NT>
 int launch_ci16_dot2(DecimLaunch L, int channels, bool mixed, hipStream_t s) {
+#ifdef SRCDSP_TUNING
     switch (ci16_variant()) {
     case 0: return launch_ci16_dot2_shape<NT, 256, 0>(L, channels, mixed, s);
     case 1: return launch_ci16_dot2_shape<NT, 512, 0>(L, channels, mixed, s);
     case 2: return launch_ci16_dot2_shape<NT, 256, 1>(L, channels, mixed, s);
     case 3: return launch_ci16_dot2_shape<NT, 512, 1>(L, channels, mixed, s);
-    default:
-        // the sequence table (conflict-free reads for any frequency) when its
-        // period fits the LDS budget, else the doubled phase table
-        if (mixed && mixer_seq_period(L.mix_N, L.mix_freq) > kSeqMax)
-            return launch_ci16_dot2_shape<NT, 512, 1>(L, channels, mixed, s);
-        return launch_ci16_dot2_shape<NT, 512, 2>(L, channels, mixed, s);
+    default: break;
     }
+#endif
+    // the product shape: 512 lanes; the sequence mixer table (conflict-free
+    // reads for any frequency) when its period fits the LDS budget, else the
+    // doubled phase table (only these instantiations are compiled outside the
+    // tuning build)
+    if (mixed && mixer_seq_period(L.mix_N, L.mix_freq) > kSeqMax)
+        return launch_ci16_dot2_shape<NT, 512, 1>(L, channels, mixed, s);
+    return launch_ci16_dot2_shape<NT, 512, 2>(L, channels, mixed, s);
 }
 
 template <int KV>
