@@ -251,7 +251,7 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
     } else if (f.M == 1 && (f.kv == KV_CF32 || f.kv == KV_F32_REAL) && al && out_al && f.ntaps <= kFirMaxTaps && !mixed) {
         rc = f.kv == KV_CF32 ? launch_fir_tile<KV_CF32>(L, channels, fma, s)
                              : launch_fir_tile<KV_F32_REAL>(L, channels, fma, s);
-    } else if (f.M == 4 && f.kv == KV_CF32 && al &&
+    } else if (f.M == 4 && f.kv == KV_CF32 && al && out_al &&
                (f.ntaps == 63 || f.ntaps == 64 || f.ntaps == 127 || f.ntaps == 128 || f.ntaps == 255 || f.ntaps == 256)) {
         // the headline kernel, compiled per tap count: 127/128 (BASELINE configs 2 and
         // 3) and the neighbouring power-of-two lengths
@@ -263,39 +263,39 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
         case 255: rc = launch_cf32<255>(L, channels, fma, s); break;
         default: rc = launch_cf32<256>(L, channels, fma, s); break;
         }
-    } else if (f.M == 2 && f.kv == KV_CF32 && al && (f.ntaps == 63 || f.ntaps == 64 || f.ntaps == 127 || f.ntaps == 128)) {
+    } else if (f.M == 2 && f.kv == KV_CF32 && al && out_al && (f.ntaps == 63 || f.ntaps == 64 || f.ntaps == 127 || f.ntaps == 128)) {
         switch (f.ntaps) {
         case 63: rc = launch_cf32<63, 2>(L, channels, fma, s); break;
         case 64: rc = launch_cf32<64, 2>(L, channels, fma, s); break;
         case 127: rc = launch_cf32<127, 2>(L, channels, fma, s); break;
         default: rc = launch_cf32<128, 2>(L, channels, fma, s); break;
         }
-    } else if (f.M == 3 && f.kv == KV_CF32 && al && (f.ntaps == 63 || f.ntaps == 64 || f.ntaps == 127 || f.ntaps == 128)) {
+    } else if (f.M == 3 && f.kv == KV_CF32 && al && out_al && (f.ntaps == 63 || f.ntaps == 64 || f.ntaps == 127 || f.ntaps == 128)) {
         switch (f.ntaps) {
         case 63: rc = launch_cf32<63, 3>(L, channels, fma, s); break;
         case 64: rc = launch_cf32<64, 3>(L, channels, fma, s); break;
         case 127: rc = launch_cf32<127, 3>(L, channels, fma, s); break;
         default: rc = launch_cf32<128, 3>(L, channels, fma, s); break;
         }
-    } else if (f.M == 16 && f.kv == KV_CF32 && al && (f.ntaps == 127 || f.ntaps == 128 || f.ntaps == 255 || f.ntaps == 256)) {
+    } else if (f.M == 16 && f.kv == KV_CF32 && al && out_al && (f.ntaps == 127 || f.ntaps == 128 || f.ntaps == 255 || f.ntaps == 256)) {
         switch (f.ntaps) {
         case 127: rc = launch_cf32<127, 16>(L, channels, fma, s); break;
         case 128: rc = launch_cf32<128, 16>(L, channels, fma, s); break;
         case 255: rc = launch_cf32<255, 16>(L, channels, fma, s); break;
         default: rc = launch_cf32<256, 16>(L, channels, fma, s); break;
         }
-    } else if (f.M == 8 && f.kv == KV_CF32 && al && (f.ntaps == 127 || f.ntaps == 128 || f.ntaps == 255 || f.ntaps == 256)) {
+    } else if (f.M == 8 && f.kv == KV_CF32 && al && out_al && (f.ntaps == 127 || f.ntaps == 128 || f.ntaps == 255 || f.ntaps == 256)) {
         switch (f.ntaps) {
         case 127: rc = launch_cf32<127, 8>(L, channels, fma, s); break;
         case 128: rc = launch_cf32<128, 8>(L, channels, fma, s); break;
         case 255: rc = launch_cf32<255, 8>(L, channels, fma, s); break;
         default: rc = launch_cf32<256, 8>(L, channels, fma, s); break;
         }
-    } else if (f.M == 4 && f.kv == KV_CI16_I32 && f.coef_fits_i16 && al && (f.ntaps == 127 || f.ntaps == 128)) {
+    } else if (f.M == 4 && f.kv == KV_CI16_I32 && f.coef_fits_i16 && al && out_al && (f.ntaps == 127 || f.ntaps == 128)) {
         DecimLaunch L2 = L;
         L2.coef = f.d_cpair;
         rc = f.ntaps == 127 ? launch_ci16_dot2<127>(L2, channels, mixed, s) : launch_ci16_dot2<128>(L2, channels, mixed, s);
-    } else if (f.M == 4 && f.kv == KV_CI16_I32 && f.coef_fits_i16 && al && !mixed &&
+    } else if (f.M == 4 && f.kv == KV_CI16_I32 && f.coef_fits_i16 && al && out_al && !mixed &&
                (f.ntaps == 63 || f.ntaps == 64 || f.ntaps == 255 || f.ntaps == 256)) {
         // the dot2 kernel's product shape at the neighbouring power-of-two lengths
         DecimLaunch L2 = L;
@@ -306,7 +306,7 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
         case 255: rc = launch_ci16_dot2_shape<255, 512, 0>(L2, channels, false, s); break;
         default: rc = launch_ci16_dot2_shape<256, 512, 0>(L2, channels, false, s); break;
         }
-    } else if (f.M == 4 && f.kv == KV_CI16_I32 && f.coef_fits_i24 && al && (f.ntaps == 127 || f.ntaps == 128)) {
+    } else if (f.M == 4 && f.kv == KV_CI16_I32 && f.coef_fits_i24 && al && out_al && (f.ntaps == 127 || f.ntaps == 128)) {
         rc = f.ntaps == 127 ? launch_ci16<127>(L, channels, mixed, s) : launch_ci16<128>(L, channels, mixed, s);
     } else if ((f.kv == KV_CF32 || f.kv == KV_CI16_I32 || f.kv == KV_CI16_I16) &&
                (f.M <= 6 || f.M == 8 || f.M == 16) &&
@@ -324,7 +324,7 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
             rc = launch_decim_tile_m<KV_CI16_I32, 1>(L, channels, f.M, s);
     } else {
         if (mixed) {
-            set_error("mixer->decimator fusion needs variant 1, M=4, 127/128 taps |c|<2^23, 16-B aligned input");
+            set_error("mixer->decimator fusion needs variant 1, M=4, 127/128 taps |c|<2^23, 16-B aligned input and output");
             return SRCDSP_ERR_UNSUPPORTED;
         }
         switch (f.kv) {

@@ -341,6 +341,46 @@ def test_decim_generic_paths_vs_oracle(S, O):
     del torch
 
 
+@pytest.mark.parametrize("M,ntaps", [(4, 127), (4, 255), (2, 63), (3, 128), (8, 255), (16, 127), (1, 127), (1, 300)])
+def test_decim_cf32_misaligned_views_vs_oracle(S, O, M, ntaps):
+    """Caller-supplied input / output views that are 8-B but not 16-B aligned
+    at every tuned complex<float> shape: the 16-B-store kernels must not take
+    them (they fall back to the generic path), results stay bit-exact."""
+    import torch
+    from srcdsp_amd.design import hamming_sinc
+    c = hamming_sinc(ntaps, 0.4 / M)
+    n = 6000 * M
+    x = O["fma"].gen_cf32(11 + M, 0, 0, n + 1)
+    for in_off, out_off in [(0, 1), (1, 0), (1, 1)]:
+        g, r = S.FilterDnsamplingFir(c, M), O["fma"].decim(0, M, c)
+        xin = dev(x)[in_off:in_off + n]
+        obuf = torch.zeros(n // M + 1, dtype=torch.complex64, device="cuda")
+        for rep in range(2):  # history carried across the fallback
+            y = obuf[out_off:out_off + n // M]
+            g.step(xin, y)
+            exp = r.step(x[in_off:in_off + n])
+            assert np.array_equal(y.cpu().numpy().view(np.uint32), exp.view(np.uint32)), (in_off, out_off, rep)
+        if out_off:
+            assert obuf[0].item() == 0  # nothing written before the view
+
+
+@pytest.mark.parametrize("ntaps", [127, 255])
+def test_decim_ci16_misaligned_output_vs_oracle(S, O, ntaps):
+    """complex<int16_t> outputs into a 4-B-offset view: the dot2 / mad24
+    kernels' 16-B stores are not taken; bit-exact through the fallback."""
+    import torch
+    rng = np.random.default_rng(ntaps)
+    c = rng.integers(-3000, 3000, ntaps).astype(np.int32)
+    n = 4 * 5000
+    x = O["fma"].gen_ci16(99, 0, 0, n, -32768, 32767)
+    g, r = S.FilterDnsamplingFir(c, 4, "complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int32_t"), O["fma"].decim(1, 4, c)
+    obuf = torch.zeros((n // 4 + 1, 2), dtype=torch.int16, device="cuda")
+    for rep in range(2):
+        y = obuf[1:1 + n // 4]
+        g.step(dev(x), y)
+        assert np.array_equal(y.cpu().numpy(), r.step(x)), rep
+
+
 def test_decim_errors_and_empty(S):
     import torch
     from srcdsp_amd._capi import ERR_SIZE, SrcdspError
