@@ -702,27 +702,45 @@ SRCDSP_API int srcdsp_fir_step_host(srcdsp_fir_t h, const void *in, size_t n_in,
 }
 
 // -------------------------------------------------- Mixer -> decimator chain
+// The two reference calls as two launches, through a stream-ordered scratch
+// buffer: the configurations the fused kernel does not cover.
+static int mixdecim_unfused(srcdsp_mixer_t mixer, FirCore &f, const void *d_in, size_t n_in, void *d_out,
+                            size_t n_out, hipStream_t s) {
+    void *tmp = nullptr;
+    SRCDSP_HIP_TRY(hipMallocAsync(&tmp, n_in * 4, s));
+    int rc = srcdsp_mixer_step(mixer, d_in, n_in, tmp, s);  // mixers.h:169-188
+    if (rc == SRCDSP_OK) rc = core_step(f, tmp, n_in, d_out, n_out, s, nullptr);
+    const hipError_t e = hipFreeAsync(tmp, s);
+    if (rc == SRCDSP_OK && e != hipSuccess) {
+        set_error(std::string("mixdecim_step: ") + hipGetErrorString(e));
+        return SRCDSP_ERR_HIP;
+    }
+    return rc;
+}
+
 SRCDSP_API int srcdsp_mixdecim_step(srcdsp_mixer_t mixer, srcdsp_decim_t decim, const void *d_in, size_t n_in,
                                     void *d_out, size_t n_out, void *stream) {
     SRCDSP_ARG_CHECK(mixer != nullptr && decim != nullptr, "mixdecim_step: null handle");
     FirCore &f = decim->core;
     MixerState &m = mixer->m;
-    if (f.kv != KV_CI16_I32) {
-        set_error("mixdecim_step: the decimator must be variant 1 (ci16 x int32 taps)");
-        return SRCDSP_ERR_UNSUPPORTED;
-    }
-    if (m.N > 4096) {
-        set_error("mixdecim_step: fused mixer table limited to N <= 4096");
+    if (f.kv != KV_CI16_I32 && f.kv != KV_CI16_I16) {
+        set_error("mixdecim_step: the decimator must take complex<int16_t> input (the mixer's output)");
         return SRCDSP_ERR_UNSUPPORTED;
     }
     if (n_out * f.M != n_in) {
         set_error("mixdecim_step: out.size()*M != in.size() (dnsampling_filters.h:133)");
         return SRCDSP_ERR_SIZE;
     }
+    if (n_in == 0) return SRCDSP_OK;
+    SRCDSP_ARG_CHECK(d_in && d_out, "mixdecim_step: null buffer");
     hipStream_t s = (hipStream_t)stream;
+    // fused: variant 1, M = 4, 127/128 taps with |c| < 2^23, a table of <= 4096
+    // entries, 16-B aligned buffers (decim_launch refuses the rest unchanged)
+    if (f.kv != KV_CI16_I32 || m.N > 4096) return mixdecim_unfused(mixer, f, d_in, n_in, d_out, n_out, s);
     int rc = m.order.before(s);
     if (rc) return rc;
     rc = core_step(f, d_in, n_in, d_out, n_out, s, &m);
+    if (rc == SRCDSP_ERR_UNSUPPORTED) return mixdecim_unfused(mixer, f, d_in, n_in, d_out, n_out, s);
     if (rc) return rc;
     // mixer phase after the call: phi += n_in * freq (mod N), mixers.h:177
     m.phi = (int16_t)(((unsigned long)(unsigned)m.phi + (unsigned long)(n_in % m.N) * (unsigned)m.freq) % m.N);

@@ -277,6 +277,56 @@ def test_mixdecim_chain_table_sizes(S, O, N, f):
         assert m.state()[:2] == om.state()[:2]
 
 
+@pytest.mark.parametrize("case", ["m2", "t63", "t16taps", "wide_taps", "n8192", "out_offset", "in_offset"])
+def test_mixdecim_chain_unfused_configs(S, O, case):
+    """Chain configurations the fused kernel does not cover run as the two
+    reference calls (mixer launch into a stream-ordered scratch buffer, then the
+    decimator): M = 2, 63 taps, int16 taps (variant 2), taps beyond 2^23, a
+    table of 8192 entries, 4-B-offset output / input views.  Same outputs and
+    the same mixer and decimator state as the two oracle calls."""
+    import torch
+    from srcdsp_amd.design import hamming_sinc, q14
+    M, ntaps, N, variant = 4, 127, 4096, 1
+    if case == "m2":
+        M = 2
+    elif case == "t63":
+        ntaps = 63
+    elif case == "t16taps":
+        variant = 2
+    elif case == "n8192":
+        N = 8192
+    cq = q14(hamming_sinc(ntaps))
+    if case == "wide_taps":
+        cq = cq.astype(np.int64) * 1024
+        cq[0] = 1 << 24
+        cq = cq.astype(np.int32)
+    ctype = "int16_t" if variant == 2 else "int32_t"
+    if variant == 2:
+        cq = cq.astype(np.int16)
+    x = O["strict"].gen_ci16(0xC0DE, 5, 0, 300001, -32768, 32767)
+    m = S.Mixer(N)
+    m.reset(0.13)
+    d = S.FilterDnsamplingFir(cq, M, "complex<int16_t>", "complex<int16_t>", "complex<int32_t>", ctype)
+    chain = S.MixerDecimatorChain(m, d)
+    om, od = O["strict"].mixer(N), O["strict"].decim(variant, M, cq)
+    om.reset(0.13)
+    xd = dev(x)
+    for off, n in _chunks(300000, [131072, 8, 4100, 200000]):
+        n -= n % M
+        if n == 0:
+            continue
+        ioff = 1 if case == "in_offset" else 0
+        xs = x[off + ioff:off + ioff + n]
+        if case == "out_offset":
+            obuf = torch.zeros((n // M + 1, 2), dtype=torch.int16, device="cuda")
+            y = chain.step(xd[off:off + n], obuf[1:])
+            assert not obuf[0].any()
+        else:
+            y = chain.step(xd[off + ioff:off + ioff + n])
+        assert np.array_equal(y.cpu().numpy(), od.step(om.step(xs))), (case, off, n)
+        assert m.state()[:2] == om.state()[:2]
+
+
 @pytest.mark.parametrize("fp", ["fma", "strict"])
 @pytest.mark.parametrize("ntaps", [1, 2, 3, 5, 12, 13, 31, 127, 1000, 1030])
 def test_fir_float_tile_kernel_vs_oracle(S, O, fp, ntaps):
