@@ -151,10 +151,12 @@ def test_fuzz_mixer_and_chain(S, O, seed):
     fused = bool(rng.integers(0, 2))
     if fused:
         from srcdsp_amd.design import hamming_sinc, q14
-        cq = q14(hamming_sinc(int(rng.choice([127, 128])), 0.12))
-        d = S.FilterDnsamplingFir(cq, 4, *_DECIM_T[1])
+        # M = 4 x 127/128 is the fused kernel; the others run as the two calls
+        Md = int(rng.choice([4, 4, 4, 2, 8]))
+        cq = q14(hamming_sinc(int(rng.choice([127, 128, 63])), 0.12))
+        d = S.FilterDnsamplingFir(cq, Md, *_DECIM_T[1])
         chain = S.MixerDecimatorChain(m, d)
-        od = O["fma"].decim(1, 4, cq)
+        od = O["fma"].decim(1, Md, cq)
     for op in range(8):
         u = rng.random()
         if u < 0.15:
@@ -165,7 +167,7 @@ def test_fuzz_mixer_and_chain(S, O, seed):
             f = float(rng.uniform(-1, 1))
             m.setFrequency(f)
             om.set_frequency(f)
-        n = 4 * int(rng.choice([0, 1, 7, 1000, 4097, int(rng.integers(0, 20000))]))
+        n = 8 * int(rng.choice([0, 1, 7, 1000, 4097, int(rng.integers(0, 20000))]))
         x = O["fma"].gen_ci16(int(rng.integers(1 << 30)), 0, 0, n, -32768, 32767)
         if fused:
             got = chain.step(_dev(x)).cpu().numpy()
