@@ -678,6 +678,54 @@ def test_upsampler_dot2_kernel_vs_oracle(S, O, L, H):
         r.reset()
 
 
+@pytest.mark.parametrize("in_off,out_off", [(1, 0), (0, 1), (1, 1), (2, 2)])
+def test_offset_views_up_mixer_corr(S, O, in_off, out_off):
+    """Upsampler (the dot2 shape L = 4 x 128 and the wide-tap tile kernel),
+    mixer and correlator on device views 4-B (one complex<int16_t>) off
+    16-B alignment: the vector kernels are not taken for them, results stay
+    bit-exact and the state carries over to aligned calls."""
+    import torch
+    from srcdsp_amd.design import qpsk_pattern
+    rng = np.random.default_rng(in_off * 10 + out_off)
+    n = 20001
+    x = O["fma"].gen_ci16(3 + in_off, 0, 0, n + 4, -32768, 32767)
+    xd = dev(x)
+    for c in (rng.integers(-32768, 32768, 128), rng.integers(-(1 << 24), 1 << 24, 128)):
+        g, r = S.FilterUpsamplingFir(c, 4, *_UP_TYPES[0]), O["fma"].up(0, 4, c)
+        for k, (a, b) in enumerate([(0, 7000), (7000, n)]):
+            xs = xd[a + in_off:b + in_off] if k == 0 else xd[a:b]  # offset view, then aligned
+            obuf = torch.zeros((4 * (b - a) + out_off, 2), dtype=torch.int16, device="cuda")
+            y = obuf[out_off:] if k == 0 else obuf[:4 * (b - a)]
+            g.step(xs, y)
+            exp = r.step(x[a + in_off:b + in_off] if k == 0 else x[a:b])
+            assert np.array_equal(y.cpu().numpy(), exp), (k, c[0])
+    m, om = S.Mixer(4096), O["fma"].mixer(4096)
+    m.reset(0.21)
+    om.reset(0.21)
+    for k, (a, b) in enumerate([(0, 10000), (10000, n)]):
+        xs = xd[a + in_off:b + in_off] if k == 0 else xd[a:b]
+        obuf = torch.zeros((b - a + out_off, 2), dtype=torch.int16, device="cuda")
+        y = obuf[out_off:] if k == 0 else obuf[:b - a]
+        m.step(xs, y)
+        exp = om.step(x[a + in_off:b + in_off] if k == 0 else x[a:b])
+        assert np.array_equal(y.cpu().numpy(), exp), k
+        assert m.state()[:2] == om.state()[:2]
+    p = qpsk_pattern(64, 500, seed=3)
+    xc = rng.integers(-125, 126, size=(n + 4, 2))
+    xc[12000:12000 + 64] += 2 * p
+    xc = np.clip(xc, -32768, 32767).astype(np.int16)
+    g, r = S.FixedPatternCorrelator(64, 1), O["fma"].corr(64, 1)
+    g.setPattern(p)
+    r.set_pattern(p)
+    xcd = dev(xc)
+    for k, (a, b) in enumerate([(0, 5000), (5000, n)]):
+        xs = xcd[a + in_off:b + in_off] if k == 0 else xcd[a:b]
+        fg, ig = g.step(xs)
+        fr, ir = r.step(xc[a + in_off:b + in_off] if k == 0 else xc[a:b])
+        assert (fg, fg and ig) == (fr, fr and ir), (k, fg, ig, fr, ir)
+        assert np.array_equal(g.getRefBitSamples(), r.bit_samples())
+
+
 @pytest.mark.parametrize("N,S_", [(1024, 1), (32, 4), (64, 2)])
 def test_correlator_vs_oracle(S, O, N, S_):
     from srcdsp_amd.design import qpsk_pattern
