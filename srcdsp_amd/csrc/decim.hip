@@ -174,10 +174,20 @@ int launch_fir_tile(const DecimLaunch &L0, int channels, bool fma, hipStream_t s
     if (L.ntaps <= kFirStreamTaps) {  // persistent, prefetching
         // grid 512..2048 measure alike (0.650-0.660 ms, 2^28 samples, 31 taps); 256 is 1.7x slower
         dim3 grid((unsigned)std::min<long>(L.ntiles, kCfGridCap), channels);
-        if (fma)
-            hipLaunchKernelGGL((fir_stream_f32<KV, true>), grid, dim3(kFirBlock), 0, s, L);
-        else
-            hipLaunchKernelGGL((fir_stream_f32<KV, false>), grid, dim3(kFirBlock), 0, s, L);
+#define SRCDSP_FIR_STREAM(NTC)                                                               \
+    if (fma)                                                                                 \
+        hipLaunchKernelGGL((fir_stream_f32<KV, true, 2, NTC>), grid, dim3(kFirBlock), 0, s, L); \
+    else                                                                                     \
+        hipLaunchKernelGGL((fir_stream_f32<KV, false, 2, NTC>), grid, dim3(kFirBlock), 0, s, L)
+        // 31 taps (the reference's FilterFir example length) with the tap
+        // count compiled in; at 63 the unrolled loop spills, so longer
+        // filters keep the runtime loop
+        if (L.ntaps == 31) {
+            SRCDSP_FIR_STREAM(31);
+        } else {
+            SRCDSP_FIR_STREAM(0);
+        }
+#undef SRCDSP_FIR_STREAM
         return SRCDSP_OK;
     }
     const int span = TO + fir_halo(L.ntaps);

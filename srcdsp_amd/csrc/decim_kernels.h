@@ -1452,7 +1452,9 @@ constexpr int kFirStreamTaps = 128;
 // OST: 1 = outputs staged through LDS (two more barriers per tile); 2 = the
 // wave's outputs transposed across lanes (store_wave_lines) into whole-line
 // stores, no LDS round trip.
-template <int KV, bool FMA, int OST = 2>
+// NTC > 0: the tap count as a compile-time constant (the tap loop unrolls
+// completely); 0: a.ntaps at run time.
+template <int KV, bool FMA, int OST = 2, int NTC = 0>
 __global__ __launch_bounds__(kFirBlock, 4) void fir_stream_f32(DecimLaunch a) {
     typedef typename FirTraits<KV>::S S;
     constexpr int SPG = FirTraits<KV>::SPG;
@@ -1464,7 +1466,7 @@ __global__ __launch_bounds__(kFirBlock, 4) void fir_stream_f32(DecimLaunch a) {
     constexpr int LSTAGE = TGMAX + TGMAX / GPL + 1;
     constexpr int LOUT = TO * 8 / 16;          // output tile as float4
     __shared__ float4 fl[LSTAGE > LOUT ? LSTAGE : LOUT];
-    const int N = a.ntaps, H = N - 1;
+    const int N = NTC > 0 ? NTC : a.ntaps, H = N - 1;
     const int P0 = fir_halo(N);
     const int TG = (TO + P0) / SPG;
     const int ch = blockIdx.y;
