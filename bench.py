@@ -160,6 +160,7 @@ class Workload:
 class DecimWorkload(Workload):
     dtype = "f32"
     bytes_per_sample = 10.0  # 8 B complex<float> read + 8 B out per 4 inputs
+    read_bytes_per_sample = 8.0
 
     def __init__(self, S, torch, L, channels, rank, fp):
         from srcdsp_amd.design import hamming_sinc
@@ -183,6 +184,7 @@ class DecimWorkload(Workload):
 class MixDecimWorkload(Workload):
     dtype = "i32"
     bytes_per_sample = 5.0  # 4 B complex<int16_t> read + 4 B out per 4 inputs
+    read_bytes_per_sample = 4.0
     # algorithmic dot2 work per input sample: the decimator's 127 taps x 2
     # components per output, 1 output per 4 inputs = 63.5 int MACs = 31.75
     # v_dot2 lane-ops (the kernel issues 32: 64 tap pairs, the last with a zero
@@ -246,6 +248,7 @@ class CorrWorkload(Workload):
 class FirWorkload(Workload):
     dtype = "f32"
     bytes_per_sample = 12.0  # 4 B float in, 8 B complex<float> out
+    read_bytes_per_sample = 4.0
 
     def __init__(self, S, torch, L, channels, rank, fp):
         from srcdsp_amd.design import hamming_sinc
@@ -263,6 +266,7 @@ class UpWorkload(Workload):
     128-tap Q14 interpolator, L = 4, input length L samples -> 4L outputs."""
     dtype = "i32"
     bytes_per_sample = 20.0  # 4 B complex<int16_t> in, 4 x 4 B out per input sample
+    read_bytes_per_sample = 4.0
     # 4 outputs per input, 32 taps each, 2 components: 256 int MACs = 128 v_dot2
     # lane-ops per input sample (the kernel issues exactly these: 16 tap pairs
     # (c[2p+1], c[2p]) per phase and component)
@@ -287,6 +291,7 @@ class Ci16DecimWorkload(Workload):
     127 Q14 taps, no mixer (config 4's decimator)."""
     dtype = "i32"
     bytes_per_sample = 5.0
+    read_bytes_per_sample = 4.0
     dot2_per_sample = 31.75  # 127 taps x 2 components / 4 = 63.5 int MACs (the kernel issues 32 dot2)
 
     def __init__(self, S, torch, L, channels, rank, fp):
@@ -385,9 +390,10 @@ PCIE_PEAK_GBS = 63.0  # MI355X_MICROARCH.md: host link PCIe Gen5 x16, 63 GB/s (s
 
 
 # ---------------------------------------------------------------- CPU baseline
-def cpu_baseline(args):
-    """Time the reference itself (oracle/_ref/strict, g++ -O2, 1 thread) on a
-    bounded sample of the same workload; test infrastructure, never the product."""
+def cpu_baseline(args, flavour="strict", sample=None):
+    """Time the reference itself (oracle/_ref/<flavour>: strict = g++ -O2, O0 =
+    the reference makefile's own flags, no -O; 1 thread) on a bounded sample
+    of the same workload; test infrastructure, never the product."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     from srcdsp_amd.design import hamming_sinc
@@ -395,9 +401,11 @@ def cpu_baseline(args):
         return cpu_baseline_other(args, pyoracle)
     if args.workload != "decim":
         return None
-    d = os.path.join(ROOT, "oracle", "_ref", "strict")
+    d = os.path.join(ROOT, "oracle", "_ref", flavour)
     path = os.path.join(d, "libref_decim_old.so")
-    n = min(args.cpu_sample, args.samples)
+    if flavour != "strict" and not os.path.exists(path):
+        return None
+    n = min(sample or args.cpu_sample, args.samples)
     n -= n % 4
     if os.path.exists(path):
         lib = C.CDLL(path)
@@ -413,7 +421,9 @@ def cpu_baseline(args):
         secs = lib.ref_decim_step_timed(h, x.ctypes.data, n, y.ctypes.data)
         lib.ref_decim_destroy(h)
         kind = "reference"
-        src = "oracle/_ref/strict/libref_decim_old.so (dnsampling_filters.h built g++ -O2, x86-64 baseline)"
+        src = (f"oracle/_ref/{flavour}/libref_decim_old.so (dnsampling_filters.h built g++ "
+               + ("-O2, x86-64 baseline)" if flavour == "strict" else
+                  "-std=gnu++11 without -O: the reference makefile's flags, /root/reference/makefile:18)"))
     else:  # no reference build travelled: time the C restatement instead
         o = pyoracle.Oracle(0)
         x = o.gen_cf32(SEED, 0, 0, n)
@@ -695,6 +705,14 @@ def main():
     if args.workload in ("up", "fifo", "iq"):
         per_launch_samples = work.n
     achieved = work.bytes_per_sample * per_launch_samples / (kern_avg_ms * 1e-3) / 1e9
+    # SURVEY 8d / north_star: the input-read stream alone against the HBM peak
+    # ("HBM-read roofline"), beside `roofline` (which counts reads + writes)
+    rb = getattr(work, "read_bytes_per_sample", None)
+    hbm_read = None
+    if rb and getattr(work, "bound", "hbm") == "hbm":
+        rd = rb * per_launch_samples / (kern_avg_ms * 1e-3) / 1e9
+        hbm_read = {"achieved": round(rd, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(rd / HBM_PEAK_GBS, 4),
+                    "read_bytes_per_launch": int(rb * per_launch_samples), "kernel_ms": round(kern_avg_ms, 4)}
     traffic, traffic_note = pmc_traffic(args, work.name, per_launch_samples)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_note,
@@ -752,7 +770,7 @@ def main():
                 "scaling": "strong" if args.workload == "corr" and world > 1 else "weak",
                 "vs_baseline": None, "dtype": work.dtype,
                 "data": "synthetic (counter-based splitmix64 integer samples, SURVEY §8d)", "config": cfg,
-                "roofline": roof, "world_size_reported": reported,
+                "roofline": roof, "hbm_read": hbm_read, "world_size_reported": reported,
                 "backend": BACKEND if world > 1 else None}
         if gather_ms is not None:
             line["gather_ms"] = round(gather_ms, 3)
@@ -763,6 +781,8 @@ def main():
             line["cpu_baseline"] = cpu_baseline(args)
             if args.workload == "decim":
                 line["cpu_baseline_allcores"] = cpu_baseline_allcores(args)
+                # the reference-equivalent -O0 build, for context
+                line["cpu_baseline_O0"] = cpu_baseline(args, "O0", sample=1 << 24)
         if args.workload == "decim" and world == 1 and not args.no_pcie:
             line["pcie_inclusive"] = pcie_inclusive(S)
         print(json.dumps(line), flush=True)

@@ -45,8 +45,15 @@ public:
         srcdsp_detail::check(srcdsp_corr_create(&h_, (unsigned)N, (unsigned)S), "FixedPatternCorrelator");
     }
     ~FixedPatternCorrelator() { srcdsp_corr_destroy(h_); }
-    FixedPatternCorrelator(const FixedPatternCorrelator &) = delete;
-    FixedPatternCorrelator &operator=(const FixedPatternCorrelator &) = delete;
+    /// copies (correlators.h:54-118 is a value type): pattern, thresholds,
+    /// history ring, registers and bitSamples
+    FixedPatternCorrelator(const FixedPatternCorrelator &o)
+        : h_(srcdsp_detail::clone_handle(o.h_, srcdsp_corr_clone, "FixedPatternCorrelator(copy)")) {}
+    FixedPatternCorrelator(FixedPatternCorrelator &&o) noexcept : h_(o.h_) { o.h_ = nullptr; }
+    FixedPatternCorrelator &operator=(FixedPatternCorrelator o) noexcept {
+        std::swap(h_, o.h_);
+        return *this;
+    }
 
     /// correlators.h:209-303
     bool step(const std::vector<std::complex<InType>> &in, int &corrIndex) {

@@ -49,17 +49,24 @@ class FilterDnsamplingFir {
 public:
     /// dsptl_dnsampling_filters.h:81-83 -- uninitialised until setCoeffs()
     FilterDnsamplingFir() : h_(nullptr) {}
-    /// dnsampling_filters.h:84-97
-    explicit FilterDnsamplingFir(const std::vector<CoefType> &firCoeff, unsigned flags = SRCDSP_DEFAULT_FLAGS)
+    /// dnsampling_filters.h:84-97 (a converting constructor, as the reference's :52)
+    FilterDnsamplingFir(const std::vector<CoefType> &firCoeff, unsigned flags = SRCDSP_DEFAULT_FLAGS)
         : h_(nullptr), flags_(flags) {
         srcdsp_detail::check(
             srcdsp_decim_create(&h_, kVariant, M, firCoeff.data(), (int)firCoeff.size(), flags_),
             "FilterDnsamplingFir");
     }
     ~FilterDnsamplingFir() { srcdsp_decim_destroy(h_); }
-    FilterDnsamplingFir(const FilterDnsamplingFir &) = delete;
-    FilterDnsamplingFir &operator=(const FilterDnsamplingFir &) = delete;
+    /// copies (dnsampling_filters.h:47-79 is a value type): coefficients,
+    /// shifts and the current history, so a copy continues the stream
+    FilterDnsamplingFir(const FilterDnsamplingFir &o)
+        : h_(srcdsp_detail::clone_handle(o.h_, srcdsp_decim_clone, "FilterDnsamplingFir(copy)")), flags_(o.flags_) {}
     FilterDnsamplingFir(FilterDnsamplingFir &&o) noexcept : h_(o.h_), flags_(o.flags_) { o.h_ = nullptr; }
+    FilterDnsamplingFir &operator=(FilterDnsamplingFir o) noexcept {  // copy-and-swap
+        std::swap(h_, o.h_);
+        std::swap(flags_, o.flags_);
+        return *this;
+    }
 
     /// dsptl_dnsampling_filters.h:114-134 (asserts N % M == 0)
     void setCoeffs(const std::vector<CoefType> &firCoeff) {

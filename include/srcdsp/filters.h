@@ -38,13 +38,19 @@ class FilterFir {
 
 public:
     FilterFir() : h_(nullptr) {}  // filters.h:49
-    explicit FilterFir(const std::vector<CoefType> &firCoeff, unsigned flags = SRCDSP_DEFAULT_FLAGS)
+    FilterFir(const std::vector<CoefType> &firCoeff, unsigned flags = SRCDSP_DEFAULT_FLAGS)
         : h_(nullptr), flags_(flags) {
         setCoeffs(firCoeff);
     }
     ~FilterFir() { srcdsp_fir_destroy(h_); }
-    FilterFir(const FilterFir &) = delete;
-    FilterFir &operator=(const FilterFir &) = delete;
+    /// copies (filters.h:42-70 is a value type): taps, shift, history
+    FilterFir(const FilterFir &o) : h_(dsptl::srcdsp_detail::clone_handle(o.h_, srcdsp_fir_clone, "FilterFir(copy)")), flags_(o.flags_) {}
+    FilterFir(FilterFir &&o) noexcept : h_(o.h_), flags_(o.flags_) { o.h_ = nullptr; }
+    FilterFir &operator=(FilterFir o) noexcept {
+        std::swap(h_, o.h_);
+        std::swap(flags_, o.flags_);
+        return *this;
+    }
 
     /// filters.h:131-169 ; filteredSignal.size() == signal.size()
     void step(const std::vector<InType> &signal, std::vector<OutType> &filteredSignal) {

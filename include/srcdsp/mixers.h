@@ -19,8 +19,13 @@ public:
     /// mixers.h:149-159 + _Mixer(): phi = freq = 0
     Mixer() : h_(nullptr) { srcdsp_detail::check(srcdsp_mixer_create(&h_, N), "Mixer"); }
     ~Mixer() { srcdsp_mixer_destroy(h_); }
-    Mixer(const Mixer &) = delete;
-    Mixer &operator=(const Mixer &) = delete;
+    /// copies (mixers.h:27-48 / 134-160 are value types): table, phi, freq
+    Mixer(const Mixer &o) : h_(srcdsp_detail::clone_handle(o.h_, srcdsp_mixer_clone, "Mixer(copy)")) {}
+    Mixer(Mixer &&o) noexcept : h_(o.h_) { o.h_ = nullptr; }
+    Mixer &operator=(Mixer o) noexcept {
+        std::swap(h_, o.h_);
+        return *this;
+    }
 
     /// mixers.h:51-67
     void setFrequency(float loFreq) {

@@ -15,6 +15,14 @@
  *   f.gather(d_out, out_stride, n_out, d_root, 0);     // all channels to GPU 0
  *
  * Results are those of C separate FilterDnsamplingFir objects, bit for bit.
+ *
+ * Lifetime: a ShardedDnsamplingFir holds its own reference to the
+ * communicator (srcdsp_decim_sharded_create), so the GpuComm may be destroyed
+ * before the operators built on it.
+ * Verification: run on a 1-GPU communicator only (tests/cpp/sharded_main.cpp,
+ * contiguous and strided gathers); the N > 1 step and gather paths (threaded
+ * host step, ncclGather across devices, the uneven-share ncclSend/ncclRecv
+ * loop) are unverified on hardware until a multi-GPU node runs them.
  */
 #ifndef SRCDSP_DROPIN_SHARDED_FILTERS_H
 #define SRCDSP_DROPIN_SHARDED_FILTERS_H
@@ -63,7 +71,7 @@ public:
     /// `channels` FilterDnsamplingFir(firCoeff) objects (dnsampling_filters.h:84-97)
     ShardedDnsamplingFir(GpuComm &comm, int channels, const std::vector<CoefType> &firCoeff,
                          unsigned flags = SRCDSP_DEFAULT_FLAGS)
-        : h_(nullptr), comm_(&comm), channels_(channels) {
+        : h_(nullptr), ranks_(comm.size()), channels_(channels) {
         srcdsp_detail::check(srcdsp_decim_sharded_create(&h_, comm.handle(), channels, kVariant, M, firCoeff.data(),
                                                          (int)firCoeff.size(), flags),
                              "ShardedDnsamplingFir");
@@ -96,7 +104,7 @@ public:
     /// rows in_stride / out_stride samples apart; asynchronous on the comm streams
     void step(const std::vector<const InType *> &d_in, size_t in_stride, const std::vector<OutType *> &d_out,
               size_t out_stride, size_t n_in) {
-        assert((int)d_in.size() == comm_->size() && (int)d_out.size() == comm_->size());
+        assert((int)d_in.size() == ranks_ && (int)d_out.size() == ranks_);
         std::vector<const void *> i(d_in.begin(), d_in.end());
         std::vector<void *> o(d_out.begin(), d_out.end());
         srcdsp_detail::check(srcdsp_decim_sharded_step(h_, i.data(), in_stride, o.data(), out_stride, n_in),
@@ -120,7 +128,7 @@ public:
 
 private:
     srcdsp_decim_sharded_t h_;
-    GpuComm *comm_;
+    int ranks_;
     int channels_;
 };
 

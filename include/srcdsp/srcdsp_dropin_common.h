@@ -18,6 +18,7 @@
 #include <stdexcept>
 #include <string>
 #include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "../srcdsp_hip.h"
@@ -56,6 +57,18 @@ constexpr int code4(int a, int b, int c, int d) { return ((a * 8 + b) * 8 + c) *
 template <class In, class Out, class Internal, class Coef>
 constexpr int code_of() {
     return code4(kind<In>::v, kind<Out>::v, kind<Internal>::v, kind<Coef>::v);
+}
+
+/// The reference operators are value types (implicit copy constructor and
+/// assignment over their member vectors): a copy here is a new handle with
+/// the same coefficients AND the source's current streaming state (history,
+/// phase, registers), made through the C ABI's *_clone entry.
+template <class H>
+inline H clone_handle(H h, int (*clone)(H, H *), const char *what) {
+    if (!h) return nullptr;
+    H c = nullptr;
+    check(clone(h, &c), what);
+    return c;
 }
 
 }  // namespace srcdsp_detail

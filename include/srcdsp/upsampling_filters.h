@@ -37,8 +37,14 @@ public:
         if (!firCoeff.empty()) setCoefficients(firCoeff);
     }
     ~FilterUpsamplingFir() { srcdsp_up_destroy(h_); }
-    FilterUpsamplingFir(const FilterUpsamplingFir &) = delete;
-    FilterUpsamplingFir &operator=(const FilterUpsamplingFir &) = delete;
+    /// copies (upsampling_filters.h:36-87 is a value type): taps and the history ring
+    FilterUpsamplingFir(const FilterUpsamplingFir &o)
+        : h_(srcdsp_detail::clone_handle(o.h_, srcdsp_up_clone, "FilterUpsamplingFir(copy)")) {}
+    FilterUpsamplingFir(FilterUpsamplingFir &&o) noexcept : h_(o.h_) { o.h_ = nullptr; }
+    FilterUpsamplingFir &operator=(FilterUpsamplingFir o) noexcept {
+        std::swap(h_, o.h_);
+        return *this;
+    }
 
     /// upsampling_filters.h:107-126
     void setCoefficients(const std::vector<CoefType> &firCoeff) {

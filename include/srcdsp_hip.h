@@ -78,6 +78,11 @@ typedef struct srcdsp_decim *srcdsp_decim_t;
 SRCDSP_API int srcdsp_decim_create(srcdsp_decim_t *out, int variant, unsigned M, const void *coeffs,
                                    int ntaps, unsigned flags);
 SRCDSP_API int srcdsp_decim_destroy(srcdsp_decim_t h);
+/* copy construction / assignment (the reference class is a value type: its
+ * implicit copy ctor copies coefficients, history and shifts,
+ * dnsampling_filters.h:47-79): *out = a new handle with h's coefficients,
+ * coeffScaling, leftShift and CURRENT history (after h's pending steps) */
+SRCDSP_API int srcdsp_decim_clone(srcdsp_decim_t h, srcdsp_decim_t *out);
 /* setCoeffs  dsptl_dnsampling_filters.h:114-134 (history resized, not cleared;
  * require_multiple != 0 reproduces its assert(N % M == 0) as SRCDSP_ERR_SIZE) */
 SRCDSP_API int srcdsp_decim_set_coeffs(srcdsp_decim_t h, const void *coeffs, int ntaps,
@@ -113,6 +118,8 @@ typedef struct srcdsp_fir *srcdsp_fir_t;
 SRCDSP_API int srcdsp_fir_create(srcdsp_fir_t *out, int variant, const void *coeffs, int ntaps,
                                  unsigned flags);
 SRCDSP_API int srcdsp_fir_destroy(srcdsp_fir_t h);
+/* implicit copy of FilterFir (filters.h:42-70): coefficients, shift, history */
+SRCDSP_API int srcdsp_fir_clone(srcdsp_fir_t h, srcdsp_fir_t *out);
 SRCDSP_API int srcdsp_fir_set_coeffs(srcdsp_fir_t h, const void *coeffs, int ntaps);
 /* reset  filters.h:107-113 */
 SRCDSP_API int srcdsp_fir_reset(srcdsp_fir_t h);
@@ -132,6 +139,9 @@ typedef struct srcdsp_up *srcdsp_up_t;
 /* ctor / setCoefficients  upsampling_filters.h:86-126 (ntaps % L == 0) */
 SRCDSP_API int srcdsp_up_create(srcdsp_up_t *out, int variant, unsigned L, const void *coeffs, int ntaps);
 SRCDSP_API int srcdsp_up_destroy(srcdsp_up_t h);
+/* implicit copy of FilterUpsamplingFir (upsampling_filters.h:36-87): taps,
+ * length, shift and the current history ring */
+SRCDSP_API int srcdsp_up_clone(srcdsp_up_t h, srcdsp_up_t *out);
 SRCDSP_API int srcdsp_up_set_coeffs(srcdsp_up_t h, const void *coeffs, int ntaps);
 /* reset  upsampling_filters.h:50-55 */
 SRCDSP_API int srcdsp_up_reset(srcdsp_up_t h);
@@ -152,6 +162,8 @@ typedef struct srcdsp_mixer *srcdsp_mixer_t;
 /* ctor  mixers.h:149-159 (LUT of N points), _Mixer() phi = freq = 0 */
 SRCDSP_API int srcdsp_mixer_create(srcdsp_mixer_t *out, unsigned N);
 SRCDSP_API int srcdsp_mixer_destroy(srcdsp_mixer_t h);
+/* implicit copy of Mixer (mixers.h:27-48, 134-160): table, phi, freq, nominal */
+SRCDSP_API int srcdsp_mixer_clone(srcdsp_mixer_t h, srcdsp_mixer_t *out);
 /* setFrequency / reset / adjustFrequency  mixers.h:51-98 */
 SRCDSP_API int srcdsp_mixer_set_frequency(srcdsp_mixer_t h, float lo_freq);
 SRCDSP_API int srcdsp_mixer_reset(srcdsp_mixer_t h, float lo_freq);
@@ -181,6 +193,9 @@ typedef struct srcdsp_corr *srcdsp_corr_t;
 /* ctor  correlators.h:119-132 */
 SRCDSP_API int srcdsp_corr_create(srcdsp_corr_t *out, unsigned N, unsigned S);
 SRCDSP_API int srcdsp_corr_destroy(srcdsp_corr_t h);
+/* implicit copy of FixedPatternCorrelator (correlators.h:54-118): pattern,
+ * thresholds, history ring, the three corr/energy registers, bitSamples */
+SRCDSP_API int srcdsp_corr_clone(srcdsp_corr_t h, srcdsp_corr_t *out);
 /* setPattern(array<complex<int32_t>,N>, thresholdCoeff)  correlators.h:167-194;
  * pattern = N complex<int32_t> (2N int32).  The reference's
  * assert(energy <= 1073217600) is returned as SRCDSP_ERR_ARG. */
@@ -267,6 +282,12 @@ SRCDSP_API int srcdsp_iq_load_host(const char *path, size_t component_bytes, voi
  * process by ncclCommInitAll (rccl.h:236), plus one non-blocking HIP stream
  * per device on which the sharded operators run.  `rank` below = index into
  * the device list.
+ * RCCL is loaded at the first srcdsp_comm_create (dlopen of librccl): without
+ * it that call returns SRCDSP_ERR_UNSUPPORTED, and nothing else needs RCCL.
+ * A sharded operator holds a reference to its comm: srcdsp_comm_destroy may
+ * come before srcdsp_decim_sharded_destroy.
+ * Verified on one GPU (contiguous and strided gathers); the N > 1 paths are
+ * unverified on hardware until a multi-GPU node runs them.
  * ==========================================================================*/
 typedef struct srcdsp_comm *srcdsp_comm_t;
 /* devs may be NULL (devices 0..ndev-1) */

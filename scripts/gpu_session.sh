@@ -1,0 +1,60 @@
+#!/bin/bash
+# One GPU session (the single session script; earlier rounds' one-off scripts
+# are folded into these steps).  STEPS is a space-separated list, run in
+# order; every GPU step has its own time limit, and a fault / abort / timeout
+# ends the script (no retries).  Outputs go to gpurun_out/, tagged ${TAG}.
+#
+#   smoke            __graft_entry__.py smoke
+#   tests            pytest -m gpu (PYTEST_K: -k filter)
+#   bench            bench.py ${BENCH_ARGS} (default: the headline, driver protocol --steps 20 --warmup 5)
+#   bench_all        every workload's bench line (steady protocol)
+#   prof             rocprofv3 --kernel-trace --stats of bench.py ${BENCH_ARGS} (per-dispatch CSV kept)
+#   pmc              FETCH_SIZE / WRITE_SIZE passes (scripts/pmc_traffic.py ${PMC_ARGS})
+#   ramp             cold ramps of tune variants ${VARIANTS} (scripts/tune/ramp.py), IDLE s apart
+#   envelope         scripts/shape_envelope.py ${ENV_M}
+#   census           workgroup placement census (scripts/tune/census.py)
+#   clock            in-kernel clock of a tune variant over a cold start (ramp.py, ${CLOCK_VARIANTS})
+#   dist             the 2-rank GPU test of the N > 1 path (tests/test_gpu_dist.py)
+#   cpp              the drop-in C++ tests (tests/test_dropin_cpp.py -m gpu)
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${TAG:-s}
+step() {  # step NAME SECONDS cmd...: stdout+stderr to gpurun_out/NAME.log
+  local name=$1 t=$2; shift 2
+  echo "[$name] start $(date +%T)"
+  timeout -k 10 "$t" "$@" > "gpurun_out/${name}.log" 2>&1
+  local rc=$?
+  echo "[$name] exit $rc" | tee -a gpurun_out/steps_$TAG.log
+  # 1 = test failures (keep going); anything else (fault, abort, timeout) ends the session
+  if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then echo "stopping after $name"; exit "$rc"; fi
+  return 0
+}
+for s in ${STEPS:-smoke tests bench}; do
+  case $s in
+    smoke) step smoke_$TAG 300 python -u __graft_entry__.py smoke ;;
+    tests) step tests_$TAG 1000 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread \
+             --maxfail=30 ${PYTEST_K:+-k "$PYTEST_K"} ;;
+    bench) step bench_$TAG 300 python -u bench.py ${BENCH_ARGS:---steps 20 --warmup 5} ;;
+    bench_all)
+      for w in decim mixdecim ci16decim corr fir up; do
+        step bench_${w}_$TAG 300 python -u bench.py --workload $w --no-cpu-baseline --no-pcie
+      done ;;
+    prof) step prof_$TAG 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv \
+            -- python3 bench.py --no-cpu-baseline --no-pcie ${BENCH_ARGS:---steps 20 --warmup 5} ;;
+    pmc) step pmc_$TAG 600 python -u scripts/pmc_traffic.py ${PMC_ARGS} ;;
+    ramp)
+      : > gpurun_out/ramp_$TAG.jsonl
+      for v in ${VARIANTS:-prod}; do
+        sleep ${IDLE:-8}
+        step ramp_${TAG}_$v 150 python3 -u scripts/tune/ramp.py $v ${LAUNCHES:-300}
+        tail -n 1 gpurun_out/ramp_${TAG}_$v.log >> gpurun_out/ramp_$TAG.jsonl
+      done ;;
+    envelope) step envelope_$TAG 600 python -u scripts/shape_envelope.py ${ENV_M} ;;
+    census) step census_$TAG 120 python -u scripts/tune/census.py ;;
+    dist) step dist_$TAG 300 python -u -m pytest tests/test_gpu_dist.py -m gpu -v --timeout 240 --timeout-method thread ;;
+    cpp) step cpp_$TAG 600 python -u -m pytest tests/test_dropin_cpp.py -m gpu -v --timeout 240 --timeout-method thread ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "session $TAG done"

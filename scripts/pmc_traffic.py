@@ -23,7 +23,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from srcdsp_amd.build import source_digest  # noqa: E402
-KERNEL_KEYS = {"decim": "decim_stream2_cf32", "mixdecim": "decim_dot2_ci16", "ci16decim": "decim_dot2_ci16", "corr": "corr_eval",
+KERNEL_KEYS = {"decim": "decim_stream_cf32", "mixdecim": "decim_dot2_ci16", "ci16decim": "decim_dot2_ci16", "corr": "corr_eval",
                "fir": "fir_stream_f32", "up": "up_tile"}
 BYTES_PER_SAMPLE = {"decim": 10.0, "mixdecim": 5.0, "ci16decim": 5.0, "corr": 4.0, "fir": 12.0, "up": 20.0}
 NAMES = {"decim": "decim_cf32_m4_t127", "mixdecim": "mixer4096_f0.1_to_decim_ci16_q14_m4_t127",

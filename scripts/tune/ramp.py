@@ -6,8 +6,9 @@
 
 VARIANT: a tune_decim id (70 = the product headline shape, 71 = its memory
 path only, 73 = its compute path only on L2-resident input), "prod" (the
-product library's FilterDnsamplingFir.step), "read" (read-only stream) or
-"copy" (4:1 coalesced stream).  A one-lane clock probe runs on a second
+product library's FilterDnsamplingFir.step), "w:<workload>" (one step of a
+bench.py workload: w:mixdecim, w:ci16decim, w:up, w:corr, w:fir), "read"
+(read-only stream) or "copy" (4:1 coalesced stream).  A one-lane clock probe runs on a second
 stream for the whole run; every launch's kernel time is printed with the mean
 shader clock over its span.  Run each variant in a fresh process.
 """
@@ -61,8 +62,22 @@ def main():
         seq += [v] * (int(k) if k else n)
     n = len(seq)
 
+    # bench.py workloads (the product path), built before anything is timed
+    works = {}
+    for v in set(seq):
+        if v.startswith("w:"):
+            import importlib.util
+            spec = importlib.util.spec_from_file_location("bench", os.path.join(HERE, "..", "..", "bench.py"))
+            bench = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(bench)
+            n_w = (1 << 26) if v[2:] in ("corr", "up") else (1 << 28)
+            works[v] = bench.WORKLOADS[v[2:]](S, torch, n_w, 1, 0, "fma")
+    torch.cuda.synchronize()
+
     def launch(var):
-        if var == "prod":
+        if var.startswith("w:"):  # one step of a bench.py workload, e.g. w:mixdecim
+            works[var].step()
+        elif var == "prod":
             f.step(x, y)
         elif var == "read":
             lib.tune_stream_probe2(1, 8192, C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), L, st)
@@ -83,6 +98,13 @@ def main():
         launch(seq[i])
         ev[i][1].record(main_s)
     torch.cuda.synchronize()
+    # the last launch's output against a fresh product filter (zero history,
+    # like the tuning launches): every variant must stay bit-exact
+    bitexact = None
+    if seq[-1].isdigit():
+        ref = S.FilterDnsamplingFir(c, 4).step(x)
+        torch.cuda.synchronize()
+        bitexact = bool(torch.equal(torch.view_as_real(ref).view(torch.int32), torch.view_as_real(y).view(torch.int32)))
     ms = np.array([a.elapsed_time(b) for a, b in ev])
     start_ms = np.array([ev[0][0].elapsed_time(a) for a, _ in ev])
     s = stamps.view(-1, 2).cpu().numpy().astype(np.float64)
@@ -96,7 +118,7 @@ def main():
         sel = (mid >= a) & (mid < a + d)
         ghz.append(float(np.mean(clk[sel])) if sel.any() else float("nan"))
     idle = clk[mid < -1.0]
-    out = {"variant": var, "launches": n, "seq": seq, "idle_ghz": round(float(np.median(idle)), 3) if idle.size else None,
+    out = {"variant": var, "launches": n, "bitexact_vs_product": bitexact, "idle_ghz": round(float(np.median(idle)), 3) if idle.size else None,
            "ms": [round(float(v), 4) for v in ms], "ghz": [round(v, 3) for v in ghz],
            "ms_6_25": round(float(np.mean(ms[5:25])), 4), "ms_last100": round(float(np.mean(ms[-100:])), 4),
            "ghz_6_25": round(float(np.nanmean(ghz[5:25])), 3), "ghz_last100": round(float(np.nanmean(ghz[-100:])), 3)}

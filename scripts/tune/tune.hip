@@ -1,7 +1,7 @@
 // Tuning harness (not part of the product): instantiates decimator kernel
 // variants from srcdsp_amd/csrc/decim_kernels.h and an FMA-rate microbenchmark
 // so they can be timed side by side, interleaved, in one process.
-#include "../../srcdsp_amd/csrc/decim_kernels.h"
+#include "decim_tune.h"
 #include "decim_mfma.h"
 #include "decim_ring.h"
 
@@ -106,57 +106,51 @@ extern "C" int tune_decim(int variant, int grid, const float *d_coef, const void
     auto tiles = [&](int TO) { return (L.n_out + TO - 1) / TO; };
     switch (variant) {
     // v2: buffer loads + shift-0 quantiser
-    case 10: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, false>, grid, 256, L, s);
-    case 11: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true>, grid, 256, L, s);
-    case 12: L.ntiles = tiles(128 * 4); return launch(decim_stream2_cf32<127, 4, 128, true, 4, true>, grid, 128, L, s);
-    case 13: L.ntiles = tiles(64 * 4); return launch(decim_stream2_cf32<127, 4, 64, true, 4, true>, grid, 64, L, s);
-    case 14: L.ntiles = tiles(64 * 8); return launch(decim_stream2_cf32<127, 8, 64, true, 2, true>, grid, 64, L, s);
-    case 15: L.ntiles = tiles(128 * 6); return launch(decim_stream2_cf32<127, 6, 128, true, 3, true>, grid, 128, L, s);
-    case 16: L.ntiles = tiles(64 * 6); return launch(decim_stream2_cf32<127, 6, 64, true, 3, true>, grid, 64, L, s);
-    case 20: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 1>, grid, 256, L, s);
-    case 21: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 2>, grid, 256, L, s);
-    case 22: L.ntiles = tiles(64 * 8); return launch(decim_stream2_cf32<127, 8, 64, true, 2, true, 1>, grid, 64, L, s);
-    case 23: L.ntiles = tiles(64 * 8); return launch(decim_stream2_cf32<127, 8, 64, true, 2, true, 2>, grid, 64, L, s);
-    case 30: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 0, true, false>, grid, 256, L, s);
-    case 31: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 0, false, true>, grid, 256, L, s);
-    case 32: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 0, true, true>, grid, 256, L, s);
-    case 33: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 1, true, true>, grid, 256, L, s);
-    case 34: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 0, false, false, true>, grid, 256, L, s);
-    case 35: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 0, true, false, true>, grid, 256, L, s);
-    case 36: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 0, false, true, true>, grid, 256, L, s);
-    case 37: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 0, true, true, true>, grid, 256, L, s);
-    case 38: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 1, true, true, true>, grid, 256, L, s);
-    case 40: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 0, false, false, false, true>, grid, 256, L, s);
-    case 41: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 0, true, false, false, true>, grid, 256, L, s);
-    case 42: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 0, true, true, true, true>, grid, 256, L, s);
-    case 43: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 1, false, false, false, true>, grid, 256, L, s);
-    case 44: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 0, false, true, true, true>, grid, 256, L, s);
-    case 48: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true>, grid, 512, L, s);
-    case 49: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 3, true, 0, true, true, true, true>, grid, 512, L, s);
-    case 50: L.ntiles = tiles(1024 * 4); return launch(decim_stream2_cf32<127, 4, 1024, true, 4, true, 0, true, true, true, true>, grid, 1024, L, s);
-    case 51: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, false>, grid, 512, L, s);
-    case 52: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, false, true, true, true>, grid, 512, L, s);
-    case 60: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, 2, 2>, grid, 512, L, s);
-    case 61: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, 2, 3>, grid, 512, L, s);
-    case 62: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, 3, 2>, grid, 512, L, s);
-    case 63: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, 3, 3>, grid, 512, L, s);
-    case 64: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, 18, 18>, grid, 512, L, s);
-    case 65: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, 2, 19>, grid, 512, L, s);
-    case 66: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, true, true, true, 19, 2>, grid, 512, L, s);
-    case 80: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 1, true, true, true, true>, grid, 512, L, s);
-    case 84: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 1, true, true, true, true>, grid, 256, L, s);
-    case 88: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 0, true, true, true, true>, grid, 256, L, s);
-    case 90: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 2, true, 1, true, true, true, true>, grid, 512, L, s);
+    case 10: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32_tune<127, 4, 256, true, 4, false>, grid, 256, L, s);
+    case 11: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32_tune<127, 4, 256, true, 4, true>, grid, 256, L, s);
+    case 12: L.ntiles = tiles(128 * 4); return launch(decim_stream2_cf32_tune<127, 4, 128, true, 4, true>, grid, 128, L, s);
+    case 13: L.ntiles = tiles(64 * 4); return launch(decim_stream2_cf32_tune<127, 4, 64, true, 4, true>, grid, 64, L, s);
+    case 15: L.ntiles = tiles(128 * 6); return launch(decim_stream2_cf32_tune<127, 6, 128, true, 3, true>, grid, 128, L, s);
+    case 16: L.ntiles = tiles(64 * 6); return launch(decim_stream2_cf32_tune<127, 6, 64, true, 3, true>, grid, 64, L, s);
+    case 20: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32_tune<127, 4, 256, true, 4, true, 1>, grid, 256, L, s);
+    case 21: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32_tune<127, 4, 256, true, 4, true, 2>, grid, 256, L, s);
+    case 30: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32_tune<127, 4, 256, true, 4, true, 0, true, false>, grid, 256, L, s);
+    case 31: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32_tune<127, 4, 256, true, 4, true, 0, false, true>, grid, 256, L, s);
+    case 32: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32_tune<127, 4, 256, true, 4, true, 0, true, true>, grid, 256, L, s);
+    case 33: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32_tune<127, 4, 256, true, 4, true, 1, true, true>, grid, 256, L, s);
+    case 34: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32_tune<127, 4, 256, true, 4, true, 0, false, false, true>, grid, 256, L, s);
+    case 35: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32_tune<127, 4, 256, true, 4, true, 0, true, false, true>, grid, 256, L, s);
+    case 36: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32_tune<127, 4, 256, true, 4, true, 0, false, true, true>, grid, 256, L, s);
+    case 37: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32_tune<127, 4, 256, true, 4, true, 0, true, true, true>, grid, 256, L, s);
+    case 38: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32_tune<127, 4, 256, true, 4, true, 1, true, true, true>, grid, 256, L, s);
+    case 40: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32_tune<127, 4, 256, true, 4, true, 0, false, false, false, true>, grid, 256, L, s);
+    case 41: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32_tune<127, 4, 256, true, 4, true, 0, true, false, false, true>, grid, 256, L, s);
+    case 42: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32_tune<127, 4, 256, true, 4, true, 0, true, true, true, true>, grid, 256, L, s);
+    case 43: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32_tune<127, 4, 256, true, 4, true, 1, false, false, false, true>, grid, 256, L, s);
+    case 44: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32_tune<127, 4, 256, true, 4, true, 0, false, true, true, true>, grid, 256, L, s);
+    case 48: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 0, true, true, true, true>, grid, 512, L, s);
+    case 49: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 3, true, 0, true, true, true, true>, grid, 512, L, s);
+    case 50: L.ntiles = tiles(1024 * 4); return launch(decim_stream2_cf32_tune<127, 4, 1024, true, 4, true, 0, true, true, true, true>, grid, 1024, L, s);
+    case 51: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 0, true, true, true, false>, grid, 512, L, s);
+    case 52: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 0, false, true, true, true>, grid, 512, L, s);
+    case 60: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 0, true, true, true, true, 2, 2>, grid, 512, L, s);
+    case 61: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 0, true, true, true, true, 2, 3>, grid, 512, L, s);
+    case 62: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 0, true, true, true, true, 3, 2>, grid, 512, L, s);
+    case 63: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 0, true, true, true, true, 3, 3>, grid, 512, L, s);
+    case 64: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 0, true, true, true, true, 18, 18>, grid, 512, L, s);
+    case 65: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 0, true, true, true, true, 2, 19>, grid, 512, L, s);
+    case 66: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 0, true, true, true, true, 19, 2>, grid, 512, L, s);
+    case 80: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 1, true, true, true, true>, grid, 512, L, s);
+    case 84: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32_tune<127, 4, 256, true, 4, true, 1, true, true, true, true>, grid, 256, L, s);
+    case 88: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32_tune<127, 4, 256, true, 4, true, 0, true, true, true, true>, grid, 256, L, s);
+    case 90: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 2, true, 1, true, true, true, true>, grid, 512, L, s);
     // compute path only (PROBE=2: every tile re-reads one of 16 L2-resident spans)
-    case 110: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 2, true, true, true, true>, grid, 512, L, s);
-    case 111: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 2, true, 2, true, true, true, true>, grid, 512, L, s);
-    case 112: L.ntiles = tiles(1024 * 4); return launch(decim_stream2_cf32<127, 4, 1024, true, 4, true, 2, true, true, true, true>, grid, 1024, L, s);
-    case 113: L.ntiles = tiles(1024 * 4); return launch(decim_stream2_cf32<127, 4, 1024, true, 4, true, 0, true, true, true, true>, grid, 1024, L, s);
-    case 114: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 3, true, true, true, true>, grid, 512, L, s);
-    case 120: L.ntiles = tiles(256 * 8); return launch(decim_stream2_cf32<127, 8, 256, true, 2, true, 0, true, true, true, true>, grid, 256, L, s);
-    case 121: L.ntiles = tiles(256 * 8); return launch(decim_stream2_cf32<127, 8, 256, true, 2, true, 2, true, true, true, true>, grid, 256, L, s);
-    case 122: L.ntiles = tiles(512 * 8); return launch(decim_stream2_cf32<127, 8, 512, true, 2, true, 0, true, true, true, true>, grid, 512, L, s);
-    case 123: L.ntiles = tiles(128 * 8); return launch(decim_stream2_cf32<127, 8, 128, true, 2, true, 0, true, true, true, true>, grid, 128, L, s);
+    case 110: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 2, true, true, true, true>, grid, 512, L, s);
+    case 111: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 2, true, 2, true, true, true, true>, grid, 512, L, s);
+    case 112: L.ntiles = tiles(1024 * 4); return launch(decim_stream2_cf32_tune<127, 4, 1024, true, 4, true, 2, true, true, true, true>, grid, 1024, L, s);
+    case 113: L.ntiles = tiles(1024 * 4); return launch(decim_stream2_cf32_tune<127, 4, 1024, true, 4, true, 0, true, true, true, true>, grid, 1024, L, s);
+    case 114: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 3, true, true, true, true>, grid, 512, L, s);
+    case 120: L.ntiles = tiles(256 * 8); return launch(decim_stream2_cf32_tune<127, 8, 256, true, 2, true, 0, true, true, true, true>, grid, 256, L, s);
     // OST 2: permlane32-paired whole-line stores (no LDS output staging, 2 barriers per tile)
     // matrix-core decimator (decim_mfma.h): 1024-output tiles, 2 workgroups per CU
     case 300: L.ntiles = tiles(1024); return launch(decim_mfma_cf32<127, 2, true, 0>, grid, 256, L, s);
@@ -165,26 +159,26 @@ extern "C" int tune_decim(int variant, int grid, const float *d_coef, const void
     case 303: L.ntiles = tiles(1024); return launch(decim_mfma_cf32<127, 3, true, 0>, grid, 256, L, s);
     case 304: L.ntiles = tiles(1024); return launch(decim_mfma_cf32<127, 3, true, 2>, grid, 256, L, s);
     // ILV: tap-major pk_fma issue order (inline asm)
-    case 200: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, 2, true, true, -1, -1, true>, grid, 512, L, s);
-    case 201: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 2, true, 2, true, true, -1, -1, true>, grid, 512, L, s);
-    case 202: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 2, true, 0, true, 2, true, true, -1, -1, true>, grid, 512, L, s);
-    case 203: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 0, true, 2, true, true, -1, -1, true>, grid, 256, L, s);
-    case 204: L.ntiles = tiles(512 * 8); return launch(decim_stream2_cf32<127, 8, 512, true, 2, true, 0, true, 2, true, true, -1, -1, true>, grid, 512, L, s);
-    case 70: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, 2, true, true>, grid, 512, L, s);
-    case 71: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 1, true, 2, true, true>, grid, 512, L, s);
-    case 72: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 2, true, 0, true, 2, true, true>, grid, 512, L, s);
-    case 73: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 2, true, 2, true, true>, grid, 512, L, s);
-    case 74: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32<127, 4, 256, true, 4, true, 0, true, 2, true, true>, grid, 256, L, s);
+    case 200: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 0, true, 2, true, true, -1, -1, true>, grid, 512, L, s);
+    case 201: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 2, true, 2, true, true, -1, -1, true>, grid, 512, L, s);
+    case 202: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 2, true, 0, true, 2, true, true, -1, -1, true>, grid, 512, L, s);
+    case 203: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32_tune<127, 4, 256, true, 4, true, 0, true, 2, true, true, -1, -1, true>, grid, 256, L, s);
+    case 204: L.ntiles = tiles(256 * 8); return launch(decim_stream2_cf32_tune<127, 8, 256, true, 2, true, 0, true, 2, true, true, -1, -1, true>, grid, 256, L, s);
+    case 70: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 0, true, 2, true, true>, grid, 512, L, s);
+    case 71: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 1, true, 2, true, true>, grid, 512, L, s);
+    case 72: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 2, true, 0, true, 2, true, true>, grid, 512, L, s);
+    case 73: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 2, true, 2, true, true>, grid, 512, L, s);
+    case 74: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32_tune<127, 4, 256, true, 4, true, 0, true, 2, true, true>, grid, 256, L, s);
     // 12 waves per CU: 2 x 384 lanes or 1 x 768 lanes (up to 168 VGPRs)
-    case 92: L.ntiles = tiles(384 * 4); return launch(decim_stream2_cf32<127, 4, 384, true, 3, true, 0, true, 2, true, true>, grid, 384, L, s);
-    case 93: L.ntiles = tiles(768 * 4); return launch(decim_stream2_cf32<127, 4, 768, true, 3, true, 0, true, 2, true, true>, grid, 768, L, s);
-    case 94: L.ntiles = tiles(384 * 4); return launch(decim_stream2_cf32<127, 4, 384, true, 3, true, 1, true, 2, true, true>, grid, 384, L, s);
-    case 95: L.ntiles = tiles(768 * 4); return launch(decim_stream2_cf32<127, 4, 768, true, 3, true, 1, true, 2, true, true>, grid, 768, L, s);
-    case 96: L.ntiles = tiles(384 * 4); return launch(decim_stream2_cf32<127, 4, 384, true, 4, true, 0, true, 2, true, true>, grid, 384, L, s);
-    case 76: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 4, true, 2, true, true>, grid, 512, L, s);
-    case 77: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 5, true, 2, true, true>, grid, 512, L, s);
-    case 205: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 4, true, 2, true, true, -1, -1, true>, grid, 512, L, s);
-    case 206: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 5, true, 2, true, true, -1, -1, true>, grid, 512, L, s);
+    case 92: L.ntiles = tiles(384 * 4); return launch(decim_stream2_cf32_tune<127, 4, 384, true, 3, true, 0, true, 2, true, true>, grid, 384, L, s);
+    case 93: L.ntiles = tiles(768 * 4); return launch(decim_stream2_cf32_tune<127, 4, 768, true, 3, true, 0, true, 2, true, true>, grid, 768, L, s);
+    case 94: L.ntiles = tiles(384 * 4); return launch(decim_stream2_cf32_tune<127, 4, 384, true, 3, true, 1, true, 2, true, true>, grid, 384, L, s);
+    case 95: L.ntiles = tiles(768 * 4); return launch(decim_stream2_cf32_tune<127, 4, 768, true, 3, true, 1, true, 2, true, true>, grid, 768, L, s);
+    case 96: L.ntiles = tiles(384 * 4); return launch(decim_stream2_cf32_tune<127, 4, 384, true, 4, true, 0, true, 2, true, true>, grid, 384, L, s);
+    case 76: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 4, true, 2, true, true>, grid, 512, L, s);
+    case 77: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 5, true, 2, true, true>, grid, 512, L, s);
+    case 205: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 4, true, 2, true, true, -1, -1, true>, grid, 512, L, s);
+    case 206: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 5, true, 2, true, true, -1, -1, true>, grid, 512, L, s);
     // wave-private images, no barriers (decim_wave_cf32): 256-output wave tiles
     case 400: L.ntiles = tiles(256); return launch(decim_wave_cf32<127, 512, true, 4, true>, grid, 512, L, s);
     case 401: L.ntiles = tiles(256); return launch(decim_wave_cf32<127, 256, true, 4, true>, grid, 256, L, s);
@@ -196,8 +190,7 @@ extern "C" int tune_decim(int variant, int grid, const float *d_coef, const void
     case 407: L.ntiles = tiles(256); return launch(decim_wave_cf32<127, 256, true, 4, true, 1>, grid, 256, L, s);
     case 408: L.ntiles = tiles(256); return launch(decim_wave_cf32<127, 512, true, 4, true, 1, 2, true>, grid, 512, L, s);
     case 409: L.ntiles = tiles(256); return launch(decim_wave_cf32<127, 512, true, 4, true, 0, 2, true>, grid, 512, L, s);
-    case 75: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32<127, 4, 512, true, 4, true, 0, true, 0, true, true>, grid, 512, L, s);
-    case 24: L.ntiles = tiles(128 * 8); return launch(decim_stream2_cf32<127, 8, 128, true, 2, true>, grid, 128, L, s);
+    case 75: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 0, true, 0, true, true>, grid, 512, L, s);
     // LDS-DMA loader/consumer ring (decim_ring.h): one workgroup per CU (grid 256 whatever is asked),
     // <NCONS consumer waves, NSLOT slots, NPF slots in flight, CH wave tiles per chunk>; whole chunks only
 #define RING(V, NC, NS, NP, CHK)                                                                  \
@@ -212,8 +205,26 @@ extern "C" int tune_decim(int variant, int grid, const float *d_coef, const void
     RING(504, 8, 15, 5, 8)
     RING(505, 12, 15, 3, 32)
 #undef RING
+    // round 3: the product kernel with the staging experiments (decim_stream_x<NT, R, BLOCK, MINW, STAG, EPI, PRIO>)
+    case 600: L.ntiles = tiles(512 * 4); return launch(decim_stream_x<127, 4, 512, 4, 0, 0, 0>, grid, 512, L, s);
+    case 601: L.ntiles = tiles(512 * 4); return launch(decim_stream_x<127, 4, 512, 4, 2, 0, 0>, grid, 512, L, s);
+    case 602: L.ntiles = tiles(512 * 4); return launch(decim_stream_x<127, 4, 512, 4, 4, 0, 0>, grid, 512, L, s);
+    case 603: L.ntiles = tiles(512 * 4); return launch(decim_stream_x<127, 4, 512, 4, 0, 1, 0>, grid, 512, L, s);
+    case 604: L.ntiles = tiles(512 * 4); return launch(decim_stream_x<127, 4, 512, 4, 0, 0, 1>, grid, 512, L, s);
+    case 605: L.ntiles = tiles(512 * 4); return launch(decim_stream_x<127, 4, 512, 4, 2, 1, 0>, grid, 512, L, s);
+    case 606: L.ntiles = tiles(512 * 4); return launch(decim_stream_x<127, 4, 512, 4, 0, 1, 1>, grid, 512, L, s);
+    case 607: L.ntiles = tiles(512 * 4); return launch(decim_stream_x<127, 4, 512, 4, 2, 1, 1>, grid, 512, L, s);
+    case 608: L.ntiles = tiles(256 * 4); return launch(decim_stream_x<127, 4, 256, 4, 0, 1, 0>, grid, 256, L, s);
+    case 609: L.ntiles = tiles(256 * 4); return launch(decim_stream_x<127, 4, 256, 4, 2, 1, 0>, grid, 256, L, s);
     default: return -1;
     }
+}
+
+// workgroup placement census: blocks x 512 threads, 75 KB of LDS each (the
+// headline's residency: 2 per CU); out[2 b] = HW_ID, out[2 b + 1] = XCC_ID
+extern "C" int tune_census(int blocks, unsigned *out, void *stream) {
+    hipLaunchKernelGGL(wg_census, dim3(blocks), dim3(512), 75 * 1024, (hipStream_t)stream, out);
+    return hipGetLastError();
 }
 
 // ---- FilterFir stream kernel (float in, 31 taps): output store shapes

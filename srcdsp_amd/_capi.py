@@ -26,6 +26,7 @@ FLAG_ABS_FABS, FLAG_FP_STRICT = 1, 2
 SIGNATURES = {
     "srcdsp_decim_create": (I, [HP, I, U, VP, I, U]),
     "srcdsp_decim_destroy": (I, [VP]),
+    "srcdsp_decim_clone": (I, [VP, HP]),
     "srcdsp_decim_set_coeffs": (I, [VP, VP, I, I]),
     "srcdsp_decim_set_left_shift": (I, [VP, I]),
     "srcdsp_decim_reset": (I, [VP]),
@@ -35,12 +36,14 @@ SIGNATURES = {
     "srcdsp_decim_get_state": (I, [VP, UP, IP, VP]),
     "srcdsp_fir_create": (I, [HP, I, VP, I, U]),
     "srcdsp_fir_destroy": (I, [VP]),
+    "srcdsp_fir_clone": (I, [VP, HP]),
     "srcdsp_fir_set_coeffs": (I, [VP, VP, I]),
     "srcdsp_fir_reset": (I, [VP]),
     "srcdsp_fir_step": (I, [VP, VP, SZ, VP, SZ, VP]),
     "srcdsp_fir_step_host": (I, [VP, VP, SZ, VP, SZ]),
     "srcdsp_up_create": (I, [HP, I, U, VP, I]),
     "srcdsp_up_destroy": (I, [VP]),
+    "srcdsp_up_clone": (I, [VP, HP]),
     "srcdsp_up_set_coeffs": (I, [VP, VP, I]),
     "srcdsp_up_reset": (I, [VP]),
     "srcdsp_up_get_length": (I, [VP, IP, IP, IP]),
@@ -48,6 +51,7 @@ SIGNATURES = {
     "srcdsp_up_step_host": (I, [VP, VP, SZ, VP, SZ, I, I]),
     "srcdsp_mixer_create": (I, [HP, U]),
     "srcdsp_mixer_destroy": (I, [VP]),
+    "srcdsp_mixer_clone": (I, [VP, HP]),
     "srcdsp_mixer_set_frequency": (I, [VP, F]),
     "srcdsp_mixer_reset": (I, [VP, F]),
     "srcdsp_mixer_adjust_frequency": (I, [VP, F]),
@@ -59,6 +63,7 @@ SIGNATURES = {
     "srcdsp_mixdecim_step": (I, [VP, VP, VP, SZ, VP, SZ, VP]),
     "srcdsp_corr_create": (I, [HP, U, U]),
     "srcdsp_corr_destroy": (I, [VP]),
+    "srcdsp_corr_clone": (I, [VP, HP]),
     "srcdsp_corr_set_pattern": (I, [VP, I32P, D]),
     "srcdsp_corr_reset": (I, [VP]),
     "srcdsp_corr_step": (I, [VP, VP, SZ, IP, IP, VP]),

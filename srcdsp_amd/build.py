@@ -114,9 +114,10 @@ def build(verbose: bool = False, jobs: int = 8) -> str:
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(compile_one, srcs))
     if _stale(LIB, objs):
-        # RCCL for the multi-GPU entries (multi.hip: ncclCommInitAll, ncclGather, ncclSend/Recv)
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs,
-               f"-L{ROCM_LIB}", "-lrccl", f"-Wl,-rpath,{ROCM_LIB}"]
+        # no -lrccl: multi.hip dlopens librccl at the first srcdsp_comm_create, so
+        # single-GPU users of the library neither link nor load RCCL
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs, "-ldl",
+               f"-Wl,-rpath,{ROCM_LIB}"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         r = subprocess.run(cmd, capture_output=True, text=True)

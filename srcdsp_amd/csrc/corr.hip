@@ -621,6 +621,39 @@ SRCDSP_API int srcdsp_corr_destroy(srcdsp_corr_t h) {
     return SRCDSP_OK;
 }
 
+SRCDSP_API int srcdsp_corr_clone(srcdsp_corr_t h, srcdsp_corr_t *out) {
+    SRCDSP_ARG_CHECK(h != nullptr && out != nullptr, "corr_clone: null argument");
+    *out = nullptr;
+    srcdsp_corr_state &s = h->c;
+    int rc = s.order.sync();
+    if (rc) return rc;
+    srcdsp_corr_t n = nullptr;
+    rc = srcdsp_corr_create(&n, s.N, s.S);
+    if (rc) return rc;
+    srcdsp_corr_state &c = n->c;
+    c.h_coef = s.h_coef;
+    c.taps16 = s.taps16;
+    for (int k = 0; k < 3; ++k) {
+        c.energy[k] = s.energy[k];
+        c.corr[k] = s.corr[k];
+    }
+    c.coeffs_energy = s.coeffs_energy;
+    c.coeff_scaling = s.coeff_scaling;
+    c.threshold_factor = s.threshold_factor;
+    c.bits = s.bits;
+    const size_t hb = 4 * (size_t)std::max(1u, s.NS - 1);
+    if (hipMemcpy(c.d_coef, s.d_coef, 8 * (size_t)s.N, hipMemcpyDeviceToDevice) != hipSuccess ||
+        hipMemcpy(c.d_ptaps, s.d_ptaps, 8 * (size_t)s.N, hipMemcpyDeviceToDevice) != hipSuccess ||
+        hipMemcpy(c.d_hist[0], s.d_hist[s.cur], hb, hipMemcpyDeviceToDevice) != hipSuccess) {
+        srcdsp_corr_destroy(n);
+        set_error("corr_clone: device copy failed");
+        return SRCDSP_ERR_HIP;
+    }
+    c.cur = 0;
+    *out = n;
+    return SRCDSP_OK;
+}
+
 // setPattern (correlators.h:167-194)
 SRCDSP_API int srcdsp_corr_set_pattern(srcdsp_corr_t h, const int32_t *p, double th) {
     SRCDSP_ARG_CHECK(h != nullptr && p != nullptr, "corr_set_pattern: null argument");

@@ -7,8 +7,9 @@
 // where x[<0] is the N-1 sample history carried from the previous call.
 //
 // Kernels (decim_kernels.h)
-//  * decim_stream2_cf32<NT,R,BLOCK,FMA,MINW,Q0,...> -- the headline path:
-//    complex<float>, M = 4, 127/128 taps.  A persistent grid of 512-lane
+//  * decim_stream_cf32<NT,R,BLOCK,FMA,MINW,Q0,M> -- the headline path:
+//    complex<float>, M = 4, 127 taps (and M = 1/2/3/8/16, any N <= 1024 with
+//    NT = 0: the tap count at run time).  A persistent grid of 512-lane
 //    workgroups taking tiles of BLOCK*R outputs in grid-stride order.  A
 //    tile's input span (4*BLOCK*R samples + the 4*ceil(NT/4) halo) is staged
 //    HBM -> VGPR -> LDS (non-temporal buffer_load_dwordx4, padded
@@ -53,42 +54,8 @@ namespace {
 // 75 KB LDS and 128 VGPRs = 2 resident workgroups (16 waves) per CU; the
 // persistent grid is 2x the resident capacity (measured best on MI355X:
 // scripts/tune, profiles/).
-constexpr int kCfR = 4, kCfBlock = 512, kCfGrid = 1024;
-constexpr int kCfGridCap = 2048;  // persistent grid of the other streaming kernels
+constexpr int kCfGridCap = 2048;  // persistent grid of the streaming kernels
 constexpr int kCiR = 4, kCiBlock = 256;
-
-// M = 4 is the headline; M = 8 uses the same kernel with R = 2 outputs per
-// lane (the same 16-sample lane chunks, LDS image and memory schedule), M = 2
-// with R = 4 and M = 1 (complex<float> FilterFir) with R = 8, both on 8-sample
-// lane chunks (R = 8 at M = 2 spills at the 128-VGPR budget of 16 waves per CU).
-template <int NT, int M = 4>
-int launch_cf32(DecimLaunch L, int channels, bool fma, hipStream_t s) {
-    constexpr int R = M == 1 ? 8 : (M <= 3 ? 4 : 16 / M), TO = kCfBlock * R;
-    L.ntiles = (L.n_out + TO - 1) / TO;
-    dim3 grid((unsigned)std::min<long>(L.ntiles, kCfGrid), channels);
-    const bool q0 = (L.shift & 31u) == 0;  // limitScale16 shift 0: the 4-op float quantiser
-    // measured best (scripts/tune, sustained back-to-back): 512-lane tiles
-    // (8192 samples: half the halo re-read of 256), grid-stride tile order,
-    // non-temporal input loads, outputs paired across half-waves by
-    // v_permlane32_swap into whole-line non-temporal stores (no LDS round
-    // trip: 2 barriers per tile, not 4); 2 workgroups (16 waves) per CU;
-    // taps issued tap-major through inline asm (ILV; FMA: 0.88 M instead of
-    // 1.08 M cycles per launch, -8.6 % time on one box,
-    // profiles/tuning/r02_ramp_ab.txt)
-#define SRCDSP_CF32(F, Q) \
-    hipLaunchKernelGGL((decim_stream2_cf32<NT, R, kCfBlock, F, 4, Q, 0, true, 2, true, true, -1, -1, true, M>), grid, \
-                       dim3(kCfBlock), 0, s, L)
-    if (fma && q0)
-        SRCDSP_CF32(true, true);
-    else if (fma)
-        SRCDSP_CF32(true, false);
-    else if (q0)
-        SRCDSP_CF32(false, true);
-    else
-        SRCDSP_CF32(false, false);
-#undef SRCDSP_CF32
-    return SRCDSP_OK;
-}
 
 template <int NT>
 int launch_ci16(DecimLaunch L, int channels, bool mixed, hipStream_t s) {
@@ -247,60 +214,16 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
     bool al = aligned16(L.in) && ((L.in_stride * kv_in_bytes(f.kv)) % 16 == 0);
     int rc = SRCDSP_OK;
     const bool out_al = aligned16(L.out) && ((L.out_stride * kv_out_bytes(f.kv)) % 16 == 0);
-    if (f.M == 1 && f.kv == KV_CF32 && al && out_al && !mixed &&
-        (f.ntaps == 63 || f.ntaps == 64 || f.ntaps == 127 || f.ntaps == 128)) {
-        // complex<float> single-rate FIR at the common lengths: the headline kernel
-        // with 8 outputs per lane on 8-sample lane chunks (at 255/256 taps its
-        // register window goes to scratch; those stay on fir_tile_f32)
-        switch (f.ntaps) {
-        case 63: rc = launch_cf32<63, 1>(L, channels, fma, s); break;
-        case 64: rc = launch_cf32<64, 1>(L, channels, fma, s); break;
-        case 127: rc = launch_cf32<127, 1>(L, channels, fma, s); break;
-        default: rc = launch_cf32<128, 1>(L, channels, fma, s); break;
-        }
-    } else if (f.M == 1 && (f.kv == KV_CF32 || f.kv == KV_F32_REAL) && al && out_al && f.ntaps <= kFirMaxTaps && !mixed) {
-        rc = f.kv == KV_CF32 ? launch_fir_tile<KV_CF32>(L, channels, fma, s)
-                             : launch_fir_tile<KV_F32_REAL>(L, channels, fma, s);
-    } else if (f.M == 4 && f.kv == KV_CF32 && al && out_al &&
-               (f.ntaps == 63 || f.ntaps == 64 || f.ntaps == 127 || f.ntaps == 128 || f.ntaps == 255 || f.ntaps == 256)) {
-        // the headline kernel, compiled per tap count: 127/128 (BASELINE configs 2 and
-        // 3) and the neighbouring power-of-two lengths
-        switch (f.ntaps) {
-        case 63: rc = launch_cf32<63>(L, channels, fma, s); break;
-        case 64: rc = launch_cf32<64>(L, channels, fma, s); break;
-        case 127: rc = launch_cf32<127>(L, channels, fma, s); break;
-        case 128: rc = launch_cf32<128>(L, channels, fma, s); break;
-        case 255: rc = launch_cf32<255>(L, channels, fma, s); break;
-        default: rc = launch_cf32<256>(L, channels, fma, s); break;
-        }
-    } else if (f.M == 2 && f.kv == KV_CF32 && al && out_al && (f.ntaps == 63 || f.ntaps == 64 || f.ntaps == 127 || f.ntaps == 128)) {
-        switch (f.ntaps) {
-        case 63: rc = launch_cf32<63, 2>(L, channels, fma, s); break;
-        case 64: rc = launch_cf32<64, 2>(L, channels, fma, s); break;
-        case 127: rc = launch_cf32<127, 2>(L, channels, fma, s); break;
-        default: rc = launch_cf32<128, 2>(L, channels, fma, s); break;
-        }
-    } else if (f.M == 3 && f.kv == KV_CF32 && al && out_al && (f.ntaps == 63 || f.ntaps == 64 || f.ntaps == 127 || f.ntaps == 128)) {
-        switch (f.ntaps) {
-        case 63: rc = launch_cf32<63, 3>(L, channels, fma, s); break;
-        case 64: rc = launch_cf32<64, 3>(L, channels, fma, s); break;
-        case 127: rc = launch_cf32<127, 3>(L, channels, fma, s); break;
-        default: rc = launch_cf32<128, 3>(L, channels, fma, s); break;
-        }
-    } else if (f.M == 16 && f.kv == KV_CF32 && al && out_al && (f.ntaps == 127 || f.ntaps == 128 || f.ntaps == 255 || f.ntaps == 256)) {
-        switch (f.ntaps) {
-        case 127: rc = launch_cf32<127, 16>(L, channels, fma, s); break;
-        case 128: rc = launch_cf32<128, 16>(L, channels, fma, s); break;
-        case 255: rc = launch_cf32<255, 16>(L, channels, fma, s); break;
-        default: rc = launch_cf32<256, 16>(L, channels, fma, s); break;
-        }
-    } else if (f.M == 8 && f.kv == KV_CF32 && al && out_al && (f.ntaps == 127 || f.ntaps == 128 || f.ntaps == 255 || f.ntaps == 256)) {
-        switch (f.ntaps) {
-        case 127: rc = launch_cf32<127, 8>(L, channels, fma, s); break;
-        case 128: rc = launch_cf32<128, 8>(L, channels, fma, s); break;
-        case 255: rc = launch_cf32<255, 8>(L, channels, fma, s); break;
-        default: rc = launch_cf32<256, 8>(L, channels, fma, s); break;
-        }
+    if (f.kv == KV_CF32 && al && out_al && !mixed && f.ntaps <= kCfMaxTaps &&
+        (f.M == 1 || f.M == 2 || f.M == 3 || f.M == 4 || f.M == 8 || f.M == 16)) {
+        // complex<float>: the headline kernel.  The tap count is compiled in at the
+        // BASELINE lengths (127/128: configs 2 and 3) and the common neighbouring
+        // power-of-two lengths; any other N <= 1024 takes the same kernel with
+        // the tap count at run time
+        rc = launch_cf32_compiled(L, channels, f.M, f.ntaps, fma, s);
+        if (rc == SRCDSP_ERR_UNSUPPORTED) rc = launch_cf32_rt(L, channels, f.M, fma, s);
+    } else if (f.M == 1 && f.kv == KV_F32_REAL && al && out_al && f.ntaps <= kFirMaxTaps && !mixed) {
+        rc = launch_fir_tile<KV_F32_REAL>(L, channels, fma, s);
     } else if (f.M == 4 && f.kv == KV_CI16_I32 && f.coef_fits_i16 && al && out_al && (f.ntaps == 127 || f.ntaps == 128)) {
         DecimLaunch L2 = L;
         L2.coef = f.d_cpair;
@@ -437,6 +360,22 @@ int FirCore::init(int kv_, unsigned M_, const void *coeffs, int n, unsigned flag
     return rc;
 }
 
+// a copy of the object as the reference's implicit copy constructor makes it:
+// coefficients, coeffScaling, leftShift and the current history (src settled)
+int FirCore::clone_from(FirCore &src) {
+    int rc = src.order.sync();
+    if (rc) return rc;
+    rc = init(src.kv, src.M, src.h_coef.data(), src.ntaps, src.flags);
+    if (rc) return rc;
+    left_shift = src.left_shift;
+    coeff_scaling = src.coeff_scaling;
+    if (src.ntaps > 1)
+        SRCDSP_HIP_TRY(hipMemcpy(d_hist[0], src.d_hist[src.cur], (size_t)(src.ntaps - 1) * kv_in_bytes(kv),
+                                 hipMemcpyDeviceToDevice));
+    cur = 0;
+    return SRCDSP_OK;
+}
+
 int FirCore::clear_history() {
     int rc = order.sync();
     if (rc) return rc;
@@ -549,6 +488,20 @@ SRCDSP_API int srcdsp_decim_destroy(srcdsp_decim_t h) {
     if (!h) return SRCDSP_OK;
     h->core.destroy();
     delete h;
+    return SRCDSP_OK;
+}
+
+SRCDSP_API int srcdsp_decim_clone(srcdsp_decim_t h, srcdsp_decim_t *out) {
+    SRCDSP_ARG_CHECK(h != nullptr && out != nullptr, "decim_clone: null argument");
+    *out = nullptr;
+    auto *c = new srcdsp_decim();
+    int rc = c->core.clone_from(h->core);
+    if (rc) {
+        c->core.destroy();
+        delete c;
+        return rc;
+    }
+    *out = c;
     return SRCDSP_OK;
 }
 
@@ -681,6 +634,20 @@ SRCDSP_API int srcdsp_fir_destroy(srcdsp_fir_t h) {
     return SRCDSP_OK;
 }
 
+SRCDSP_API int srcdsp_fir_clone(srcdsp_fir_t h, srcdsp_fir_t *out) {
+    SRCDSP_ARG_CHECK(h != nullptr && out != nullptr, "fir_clone: null argument");
+    *out = nullptr;
+    auto *c = new srcdsp_fir();
+    int rc = c->core.clone_from(h->core);
+    if (rc) {
+        c->core.destroy();
+        delete c;
+        return rc;
+    }
+    *out = c;
+    return SRCDSP_OK;
+}
+
 // setCoeffs (filters.h:86-97) ends in reset(): the buffer is cleared.
 SRCDSP_API int srcdsp_fir_set_coeffs(srcdsp_fir_t h, const void *coeffs, int ntaps) {
     SRCDSP_ARG_CHECK(h != nullptr, "fir_set_coeffs: null handle");
@@ -712,19 +679,28 @@ SRCDSP_API int srcdsp_fir_step_host(srcdsp_fir_t h, const void *in, size_t n_in,
 }
 
 // -------------------------------------------------- Mixer -> decimator chain
-// The two reference calls as two launches, through a stream-ordered scratch
-// buffer: the configurations the fused kernel does not cover.
+// The two reference calls as two launches, through the mixer handle's
+// grow-only scratch buffer: the configurations the fused kernel does not
+// cover.  The scratch is rewritten only after the decimator's previous step
+// (its last reader) on this stream.
 static int mixdecim_unfused(srcdsp_mixer_t mixer, FirCore &f, const void *d_in, size_t n_in, void *d_out,
                             size_t n_out, hipStream_t s) {
-    void *tmp = nullptr;
-    SRCDSP_HIP_TRY(hipMallocAsync(&tmp, n_in * 4, s));
-    int rc = srcdsp_mixer_step(mixer, d_in, n_in, tmp, s);  // mixers.h:169-188
-    if (rc == SRCDSP_OK) rc = core_step(f, tmp, n_in, d_out, n_out, s, nullptr);
-    const hipError_t e = hipFreeAsync(tmp, s);
-    if (rc == SRCDSP_OK && e != hipSuccess) {
-        set_error(std::string("mixdecim_step: ") + hipGetErrorString(e));
-        return SRCDSP_ERR_HIP;
+    MixerState &m = mixer->m;
+    if (m.scratch_cap < n_in * 4) {  // grow: only after every earlier use is done
+        int rc = f.order.sync();
+        if (!rc) rc = m.order.sync();
+        if (rc) return rc;
+        SRCDSP_HIP_TRY(hipStreamSynchronize(s));
+        if (m.d_scratch) (void)hipFree(m.d_scratch);
+        m.d_scratch = nullptr;
+        m.scratch_cap = 0;
+        SRCDSP_HIP_TRY(hipMalloc(&m.d_scratch, n_in * 4));
+        m.scratch_cap = n_in * 4;
     }
+    int rc = f.order.before(s);
+    if (rc) return rc;
+    rc = srcdsp_mixer_step(mixer, d_in, n_in, m.d_scratch, s);  // mixers.h:169-188
+    if (rc == SRCDSP_OK) rc = core_step(f, m.d_scratch, n_in, d_out, n_out, s, nullptr);
     return rc;
 }
 
@@ -750,7 +726,10 @@ SRCDSP_API int srcdsp_mixdecim_step(srcdsp_mixer_t mixer, srcdsp_decim_t decim, 
     int rc = m.order.before(s);
     if (rc) return rc;
     rc = core_step(f, d_in, n_in, d_out, n_out, s, &m);
-    if (rc == SRCDSP_ERR_UNSUPPORTED) return mixdecim_unfused(mixer, f, d_in, n_in, d_out, n_out, s);
+    if (rc == SRCDSP_ERR_UNSUPPORTED) {
+        set_error("");  // not an error: the unfused pair of launches serves this configuration
+        return mixdecim_unfused(mixer, f, d_in, n_in, d_out, n_out, s);
+    }
     if (rc) return rc;
     // mixer phase after the call: phi += n_in * freq (mod N), mixers.h:177
     m.phi = (int16_t)(((unsigned long)(unsigned)m.phi + (unsigned long)(n_in % m.N) * (unsigned)m.freq) % m.N);

@@ -43,6 +43,303 @@ __device__ __forceinline__ void pk_add_acc(f2_t &acc, f2_t p) {
     asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(acc) : "v"(p));
 }
 
+// One tap over R accumulators, skipped (by a branch inside the asm, so the
+// compiler sees straight-line code) unless k < n as unsigned, i.e. 0 <= k < n.
+// Used by the runtime-tap kernel's last chunk only.
+template <int R, bool HI, bool FMA>
+struct TapGuarded;
+
+template <>
+struct TapGuarded<1, false, true> {
+    static __device__ __forceinline__ void run(f2_t (&a)[1], unsigned long long c, const f2_t (&x)[1], int k, int n) {
+        asm volatile(
+            "s_cmp_lt_u32 %[k], %[n]\n\t"
+            "s_cbranch_scc0 1f\n\t"
+            "v_pk_fma_f32 %[a0], %[c], %[x0], %[a0] op_sel_hi:[0,1,1]\n\t"
+            "1:"
+            : [a0] "+v"(a[0])
+            : [k] "s"(k), [n] "s"(n), [c] "s"(c), [x0] "v"(x[0])
+            : "scc");
+    }
+};
+template <>
+struct TapGuarded<1, false, false> {
+    static __device__ __forceinline__ void run(f2_t (&a)[1], unsigned long long c, const f2_t (&x)[1], int k, int n) {
+        f2_t t[1];
+        asm volatile(
+            "s_cmp_lt_u32 %[k], %[n]\n\t"
+            "s_cbranch_scc0 1f\n\t"
+            "v_pk_mul_f32 %[t0], %[c], %[x0] op_sel_hi:[0,1]\n\t"
+            "v_pk_add_f32 %[a0], %[a0], %[t0]\n\t"
+            "1:"
+            : [a0] "+v"(a[0]), [t0] "=&v"(t[0])
+            : [k] "s"(k), [n] "s"(n), [c] "s"(c), [x0] "v"(x[0])
+            : "scc");
+    }
+};
+template <>
+struct TapGuarded<1, true, true> {
+    static __device__ __forceinline__ void run(f2_t (&a)[1], unsigned long long c, const f2_t (&x)[1], int k, int n) {
+        asm volatile(
+            "s_cmp_lt_u32 %[k], %[n]\n\t"
+            "s_cbranch_scc0 1f\n\t"
+            "v_pk_fma_f32 %[a0], %[c], %[x0], %[a0] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+            "1:"
+            : [a0] "+v"(a[0])
+            : [k] "s"(k), [n] "s"(n), [c] "s"(c), [x0] "v"(x[0])
+            : "scc");
+    }
+};
+template <>
+struct TapGuarded<1, true, false> {
+    static __device__ __forceinline__ void run(f2_t (&a)[1], unsigned long long c, const f2_t (&x)[1], int k, int n) {
+        f2_t t[1];
+        asm volatile(
+            "s_cmp_lt_u32 %[k], %[n]\n\t"
+            "s_cbranch_scc0 1f\n\t"
+            "v_pk_mul_f32 %[t0], %[c], %[x0] op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+            "v_pk_add_f32 %[a0], %[a0], %[t0]\n\t"
+            "1:"
+            : [a0] "+v"(a[0]), [t0] "=&v"(t[0])
+            : [k] "s"(k), [n] "s"(n), [c] "s"(c), [x0] "v"(x[0])
+            : "scc");
+    }
+};
+template <>
+struct TapGuarded<2, false, true> {
+    static __device__ __forceinline__ void run(f2_t (&a)[2], unsigned long long c, const f2_t (&x)[2], int k, int n) {
+        asm volatile(
+            "s_cmp_lt_u32 %[k], %[n]\n\t"
+            "s_cbranch_scc0 1f\n\t"
+            "v_pk_fma_f32 %[a0], %[c], %[x0], %[a0] op_sel_hi:[0,1,1]\n\t"
+            "v_pk_fma_f32 %[a1], %[c], %[x1], %[a1] op_sel_hi:[0,1,1]\n\t"
+            "1:"
+            : [a0] "+v"(a[0]), [a1] "+v"(a[1])
+            : [k] "s"(k), [n] "s"(n), [c] "s"(c), [x0] "v"(x[0]), [x1] "v"(x[1])
+            : "scc");
+    }
+};
+template <>
+struct TapGuarded<2, false, false> {
+    static __device__ __forceinline__ void run(f2_t (&a)[2], unsigned long long c, const f2_t (&x)[2], int k, int n) {
+        f2_t t[2];
+        asm volatile(
+            "s_cmp_lt_u32 %[k], %[n]\n\t"
+            "s_cbranch_scc0 1f\n\t"
+            "v_pk_mul_f32 %[t0], %[c], %[x0] op_sel_hi:[0,1]\n\t"
+            "v_pk_mul_f32 %[t1], %[c], %[x1] op_sel_hi:[0,1]\n\t"
+            "v_pk_add_f32 %[a0], %[a0], %[t0]\n\t"
+            "v_pk_add_f32 %[a1], %[a1], %[t1]\n\t"
+            "1:"
+            : [a0] "+v"(a[0]), [a1] "+v"(a[1]), [t0] "=&v"(t[0]), [t1] "=&v"(t[1])
+            : [k] "s"(k), [n] "s"(n), [c] "s"(c), [x0] "v"(x[0]), [x1] "v"(x[1])
+            : "scc");
+    }
+};
+template <>
+struct TapGuarded<2, true, true> {
+    static __device__ __forceinline__ void run(f2_t (&a)[2], unsigned long long c, const f2_t (&x)[2], int k, int n) {
+        asm volatile(
+            "s_cmp_lt_u32 %[k], %[n]\n\t"
+            "s_cbranch_scc0 1f\n\t"
+            "v_pk_fma_f32 %[a0], %[c], %[x0], %[a0] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+            "v_pk_fma_f32 %[a1], %[c], %[x1], %[a1] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+            "1:"
+            : [a0] "+v"(a[0]), [a1] "+v"(a[1])
+            : [k] "s"(k), [n] "s"(n), [c] "s"(c), [x0] "v"(x[0]), [x1] "v"(x[1])
+            : "scc");
+    }
+};
+template <>
+struct TapGuarded<2, true, false> {
+    static __device__ __forceinline__ void run(f2_t (&a)[2], unsigned long long c, const f2_t (&x)[2], int k, int n) {
+        f2_t t[2];
+        asm volatile(
+            "s_cmp_lt_u32 %[k], %[n]\n\t"
+            "s_cbranch_scc0 1f\n\t"
+            "v_pk_mul_f32 %[t0], %[c], %[x0] op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+            "v_pk_mul_f32 %[t1], %[c], %[x1] op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+            "v_pk_add_f32 %[a0], %[a0], %[t0]\n\t"
+            "v_pk_add_f32 %[a1], %[a1], %[t1]\n\t"
+            "1:"
+            : [a0] "+v"(a[0]), [a1] "+v"(a[1]), [t0] "=&v"(t[0]), [t1] "=&v"(t[1])
+            : [k] "s"(k), [n] "s"(n), [c] "s"(c), [x0] "v"(x[0]), [x1] "v"(x[1])
+            : "scc");
+    }
+};
+template <>
+struct TapGuarded<4, false, true> {
+    static __device__ __forceinline__ void run(f2_t (&a)[4], unsigned long long c, const f2_t (&x)[4], int k, int n) {
+        asm volatile(
+            "s_cmp_lt_u32 %[k], %[n]\n\t"
+            "s_cbranch_scc0 1f\n\t"
+            "v_pk_fma_f32 %[a0], %[c], %[x0], %[a0] op_sel_hi:[0,1,1]\n\t"
+            "v_pk_fma_f32 %[a1], %[c], %[x1], %[a1] op_sel_hi:[0,1,1]\n\t"
+            "v_pk_fma_f32 %[a2], %[c], %[x2], %[a2] op_sel_hi:[0,1,1]\n\t"
+            "v_pk_fma_f32 %[a3], %[c], %[x3], %[a3] op_sel_hi:[0,1,1]\n\t"
+            "1:"
+            : [a0] "+v"(a[0]), [a1] "+v"(a[1]), [a2] "+v"(a[2]), [a3] "+v"(a[3])
+            : [k] "s"(k), [n] "s"(n), [c] "s"(c), [x0] "v"(x[0]), [x1] "v"(x[1]), [x2] "v"(x[2]), [x3] "v"(x[3])
+            : "scc");
+    }
+};
+template <>
+struct TapGuarded<4, false, false> {
+    static __device__ __forceinline__ void run(f2_t (&a)[4], unsigned long long c, const f2_t (&x)[4], int k, int n) {
+        f2_t t[4];
+        asm volatile(
+            "s_cmp_lt_u32 %[k], %[n]\n\t"
+            "s_cbranch_scc0 1f\n\t"
+            "v_pk_mul_f32 %[t0], %[c], %[x0] op_sel_hi:[0,1]\n\t"
+            "v_pk_mul_f32 %[t1], %[c], %[x1] op_sel_hi:[0,1]\n\t"
+            "v_pk_mul_f32 %[t2], %[c], %[x2] op_sel_hi:[0,1]\n\t"
+            "v_pk_mul_f32 %[t3], %[c], %[x3] op_sel_hi:[0,1]\n\t"
+            "v_pk_add_f32 %[a0], %[a0], %[t0]\n\t"
+            "v_pk_add_f32 %[a1], %[a1], %[t1]\n\t"
+            "v_pk_add_f32 %[a2], %[a2], %[t2]\n\t"
+            "v_pk_add_f32 %[a3], %[a3], %[t3]\n\t"
+            "1:"
+            : [a0] "+v"(a[0]), [a1] "+v"(a[1]), [a2] "+v"(a[2]), [a3] "+v"(a[3]), [t0] "=&v"(t[0]), [t1] "=&v"(t[1]), [t2] "=&v"(t[2]), [t3] "=&v"(t[3])
+            : [k] "s"(k), [n] "s"(n), [c] "s"(c), [x0] "v"(x[0]), [x1] "v"(x[1]), [x2] "v"(x[2]), [x3] "v"(x[3])
+            : "scc");
+    }
+};
+template <>
+struct TapGuarded<4, true, true> {
+    static __device__ __forceinline__ void run(f2_t (&a)[4], unsigned long long c, const f2_t (&x)[4], int k, int n) {
+        asm volatile(
+            "s_cmp_lt_u32 %[k], %[n]\n\t"
+            "s_cbranch_scc0 1f\n\t"
+            "v_pk_fma_f32 %[a0], %[c], %[x0], %[a0] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+            "v_pk_fma_f32 %[a1], %[c], %[x1], %[a1] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+            "v_pk_fma_f32 %[a2], %[c], %[x2], %[a2] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+            "v_pk_fma_f32 %[a3], %[c], %[x3], %[a3] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+            "1:"
+            : [a0] "+v"(a[0]), [a1] "+v"(a[1]), [a2] "+v"(a[2]), [a3] "+v"(a[3])
+            : [k] "s"(k), [n] "s"(n), [c] "s"(c), [x0] "v"(x[0]), [x1] "v"(x[1]), [x2] "v"(x[2]), [x3] "v"(x[3])
+            : "scc");
+    }
+};
+template <>
+struct TapGuarded<4, true, false> {
+    static __device__ __forceinline__ void run(f2_t (&a)[4], unsigned long long c, const f2_t (&x)[4], int k, int n) {
+        f2_t t[4];
+        asm volatile(
+            "s_cmp_lt_u32 %[k], %[n]\n\t"
+            "s_cbranch_scc0 1f\n\t"
+            "v_pk_mul_f32 %[t0], %[c], %[x0] op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+            "v_pk_mul_f32 %[t1], %[c], %[x1] op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+            "v_pk_mul_f32 %[t2], %[c], %[x2] op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+            "v_pk_mul_f32 %[t3], %[c], %[x3] op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+            "v_pk_add_f32 %[a0], %[a0], %[t0]\n\t"
+            "v_pk_add_f32 %[a1], %[a1], %[t1]\n\t"
+            "v_pk_add_f32 %[a2], %[a2], %[t2]\n\t"
+            "v_pk_add_f32 %[a3], %[a3], %[t3]\n\t"
+            "1:"
+            : [a0] "+v"(a[0]), [a1] "+v"(a[1]), [a2] "+v"(a[2]), [a3] "+v"(a[3]), [t0] "=&v"(t[0]), [t1] "=&v"(t[1]), [t2] "=&v"(t[2]), [t3] "=&v"(t[3])
+            : [k] "s"(k), [n] "s"(n), [c] "s"(c), [x0] "v"(x[0]), [x1] "v"(x[1]), [x2] "v"(x[2]), [x3] "v"(x[3])
+            : "scc");
+    }
+};
+template <>
+struct TapGuarded<8, false, true> {
+    static __device__ __forceinline__ void run(f2_t (&a)[8], unsigned long long c, const f2_t (&x)[8], int k, int n) {
+        asm volatile(
+            "s_cmp_lt_u32 %[k], %[n]\n\t"
+            "s_cbranch_scc0 1f\n\t"
+            "v_pk_fma_f32 %[a0], %[c], %[x0], %[a0] op_sel_hi:[0,1,1]\n\t"
+            "v_pk_fma_f32 %[a1], %[c], %[x1], %[a1] op_sel_hi:[0,1,1]\n\t"
+            "v_pk_fma_f32 %[a2], %[c], %[x2], %[a2] op_sel_hi:[0,1,1]\n\t"
+            "v_pk_fma_f32 %[a3], %[c], %[x3], %[a3] op_sel_hi:[0,1,1]\n\t"
+            "v_pk_fma_f32 %[a4], %[c], %[x4], %[a4] op_sel_hi:[0,1,1]\n\t"
+            "v_pk_fma_f32 %[a5], %[c], %[x5], %[a5] op_sel_hi:[0,1,1]\n\t"
+            "v_pk_fma_f32 %[a6], %[c], %[x6], %[a6] op_sel_hi:[0,1,1]\n\t"
+            "v_pk_fma_f32 %[a7], %[c], %[x7], %[a7] op_sel_hi:[0,1,1]\n\t"
+            "1:"
+            : [a0] "+v"(a[0]), [a1] "+v"(a[1]), [a2] "+v"(a[2]), [a3] "+v"(a[3]), [a4] "+v"(a[4]), [a5] "+v"(a[5]), [a6] "+v"(a[6]), [a7] "+v"(a[7])
+            : [k] "s"(k), [n] "s"(n), [c] "s"(c), [x0] "v"(x[0]), [x1] "v"(x[1]), [x2] "v"(x[2]), [x3] "v"(x[3]), [x4] "v"(x[4]), [x5] "v"(x[5]), [x6] "v"(x[6]), [x7] "v"(x[7])
+            : "scc");
+    }
+};
+template <>
+struct TapGuarded<8, false, false> {
+    static __device__ __forceinline__ void run(f2_t (&a)[8], unsigned long long c, const f2_t (&x)[8], int k, int n) {
+        f2_t t[8];
+        asm volatile(
+            "s_cmp_lt_u32 %[k], %[n]\n\t"
+            "s_cbranch_scc0 1f\n\t"
+            "v_pk_mul_f32 %[t0], %[c], %[x0] op_sel_hi:[0,1]\n\t"
+            "v_pk_mul_f32 %[t1], %[c], %[x1] op_sel_hi:[0,1]\n\t"
+            "v_pk_mul_f32 %[t2], %[c], %[x2] op_sel_hi:[0,1]\n\t"
+            "v_pk_mul_f32 %[t3], %[c], %[x3] op_sel_hi:[0,1]\n\t"
+            "v_pk_mul_f32 %[t4], %[c], %[x4] op_sel_hi:[0,1]\n\t"
+            "v_pk_mul_f32 %[t5], %[c], %[x5] op_sel_hi:[0,1]\n\t"
+            "v_pk_mul_f32 %[t6], %[c], %[x6] op_sel_hi:[0,1]\n\t"
+            "v_pk_mul_f32 %[t7], %[c], %[x7] op_sel_hi:[0,1]\n\t"
+            "v_pk_add_f32 %[a0], %[a0], %[t0]\n\t"
+            "v_pk_add_f32 %[a1], %[a1], %[t1]\n\t"
+            "v_pk_add_f32 %[a2], %[a2], %[t2]\n\t"
+            "v_pk_add_f32 %[a3], %[a3], %[t3]\n\t"
+            "v_pk_add_f32 %[a4], %[a4], %[t4]\n\t"
+            "v_pk_add_f32 %[a5], %[a5], %[t5]\n\t"
+            "v_pk_add_f32 %[a6], %[a6], %[t6]\n\t"
+            "v_pk_add_f32 %[a7], %[a7], %[t7]\n\t"
+            "1:"
+            : [a0] "+v"(a[0]), [a1] "+v"(a[1]), [a2] "+v"(a[2]), [a3] "+v"(a[3]), [a4] "+v"(a[4]), [a5] "+v"(a[5]), [a6] "+v"(a[6]), [a7] "+v"(a[7]), [t0] "=&v"(t[0]), [t1] "=&v"(t[1]), [t2] "=&v"(t[2]), [t3] "=&v"(t[3]), [t4] "=&v"(t[4]), [t5] "=&v"(t[5]), [t6] "=&v"(t[6]), [t7] "=&v"(t[7])
+            : [k] "s"(k), [n] "s"(n), [c] "s"(c), [x0] "v"(x[0]), [x1] "v"(x[1]), [x2] "v"(x[2]), [x3] "v"(x[3]), [x4] "v"(x[4]), [x5] "v"(x[5]), [x6] "v"(x[6]), [x7] "v"(x[7])
+            : "scc");
+    }
+};
+template <>
+struct TapGuarded<8, true, true> {
+    static __device__ __forceinline__ void run(f2_t (&a)[8], unsigned long long c, const f2_t (&x)[8], int k, int n) {
+        asm volatile(
+            "s_cmp_lt_u32 %[k], %[n]\n\t"
+            "s_cbranch_scc0 1f\n\t"
+            "v_pk_fma_f32 %[a0], %[c], %[x0], %[a0] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+            "v_pk_fma_f32 %[a1], %[c], %[x1], %[a1] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+            "v_pk_fma_f32 %[a2], %[c], %[x2], %[a2] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+            "v_pk_fma_f32 %[a3], %[c], %[x3], %[a3] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+            "v_pk_fma_f32 %[a4], %[c], %[x4], %[a4] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+            "v_pk_fma_f32 %[a5], %[c], %[x5], %[a5] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+            "v_pk_fma_f32 %[a6], %[c], %[x6], %[a6] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+            "v_pk_fma_f32 %[a7], %[c], %[x7], %[a7] op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+            "1:"
+            : [a0] "+v"(a[0]), [a1] "+v"(a[1]), [a2] "+v"(a[2]), [a3] "+v"(a[3]), [a4] "+v"(a[4]), [a5] "+v"(a[5]), [a6] "+v"(a[6]), [a7] "+v"(a[7])
+            : [k] "s"(k), [n] "s"(n), [c] "s"(c), [x0] "v"(x[0]), [x1] "v"(x[1]), [x2] "v"(x[2]), [x3] "v"(x[3]), [x4] "v"(x[4]), [x5] "v"(x[5]), [x6] "v"(x[6]), [x7] "v"(x[7])
+            : "scc");
+    }
+};
+template <>
+struct TapGuarded<8, true, false> {
+    static __device__ __forceinline__ void run(f2_t (&a)[8], unsigned long long c, const f2_t (&x)[8], int k, int n) {
+        f2_t t[8];
+        asm volatile(
+            "s_cmp_lt_u32 %[k], %[n]\n\t"
+            "s_cbranch_scc0 1f\n\t"
+            "v_pk_mul_f32 %[t0], %[c], %[x0] op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+            "v_pk_mul_f32 %[t1], %[c], %[x1] op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+            "v_pk_mul_f32 %[t2], %[c], %[x2] op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+            "v_pk_mul_f32 %[t3], %[c], %[x3] op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+            "v_pk_mul_f32 %[t4], %[c], %[x4] op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+            "v_pk_mul_f32 %[t5], %[c], %[x5] op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+            "v_pk_mul_f32 %[t6], %[c], %[x6] op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+            "v_pk_mul_f32 %[t7], %[c], %[x7] op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+            "v_pk_add_f32 %[a0], %[a0], %[t0]\n\t"
+            "v_pk_add_f32 %[a1], %[a1], %[t1]\n\t"
+            "v_pk_add_f32 %[a2], %[a2], %[t2]\n\t"
+            "v_pk_add_f32 %[a3], %[a3], %[t3]\n\t"
+            "v_pk_add_f32 %[a4], %[a4], %[t4]\n\t"
+            "v_pk_add_f32 %[a5], %[a5], %[t5]\n\t"
+            "v_pk_add_f32 %[a6], %[a6], %[t6]\n\t"
+            "v_pk_add_f32 %[a7], %[a7], %[t7]\n\t"
+            "1:"
+            : [a0] "+v"(a[0]), [a1] "+v"(a[1]), [a2] "+v"(a[2]), [a3] "+v"(a[3]), [a4] "+v"(a[4]), [a5] "+v"(a[5]), [a6] "+v"(a[6]), [a7] "+v"(a[7]), [t0] "=&v"(t[0]), [t1] "=&v"(t[1]), [t2] "=&v"(t[2]), [t3] "=&v"(t[3]), [t4] "=&v"(t[4]), [t5] "=&v"(t[5]), [t6] "=&v"(t[6]), [t7] "=&v"(t[7])
+            : [k] "s"(k), [n] "s"(n), [c] "s"(c), [x0] "v"(x[0]), [x1] "v"(x[1]), [x2] "v"(x[2]), [x3] "v"(x[3]), [x4] "v"(x[4]), [x5] "v"(x[5]), [x6] "v"(x[6]), [x7] "v"(x[7])
+            : "scc");
+    }
+};
+
 // ------------------------------------------------------------ arithmetic
 template <bool FMA>
 __device__ __forceinline__ float mac(float c, float x, float y) {
@@ -186,32 +483,39 @@ __device__ __forceinline__ float q16f_shift0(float y) {
     return __builtin_fabsf(y) < 2147483648.0f ? t : 0.0f;
 }
 
-// Persistent complex<float> decimator, M = 4 (the headline, a1), and M = 16 / 8
-// / 3 / 2 / 1 with R = 1 / 2 / 4 / 4 / 8 outputs per lane (lane chunks of M R =
-// 16 / 16 / 12 / 8 / 8 input samples; M = 1 is the complex<float> FilterFir).
-// A tile is BLOCK*R outputs; its input span (4*BLOCK*R samples + a 4*NQ
-// sample halo, NQ = ceil(NT/4)) is staged HBM -> VGPR -> LDS as 16-B granules
-// (2 samples).  LDS granule of tile granule g:
-//   L(g) = g + (g - 2NQ + KPAD*PR) / PR,  PR = 2R granules per lane chunk,
+// Persistent complex<float> decimator: the headline (a1, M = 4, R = 4) and the
+// same schedule at M = 16 / 8 / 3 / 2 / 1 with R = 1 / 2 / 4 / 4 / 8 outputs
+// per lane (lane chunks of M R = 16 / 16 / 12 / 8 / 8 input samples; M = 1 is
+// the complex<float> FilterFir).
+//
+// Tiles.  A tile is BLOCK*R outputs; its input span (M*BLOCK*R samples + a
+// 4*NQ sample halo, NQ = ceil(N/4)) is staged HBM -> VGPR -> LDS as 16-B
+// granules (2 samples).  LDS granule of tile granule g:
+//   L(g) = g + (g - 2NQ + KPAD*PR) / PR,  PR = M*R/2 granules per lane chunk,
 // i.e. one pad granule in front of every lane chunk, so lane t's chunk starts
-// at B_t = 2NQ + KPAD + (2R+1) t and the 16 lanes of a ds_read_b128 group hit
-// 16 distinct 16-B bank slots.  Each lane owns R consecutive outputs and walks
-// the taps as 4 polyphase register windows sliding one sample per 4 taps;
-// taps are wave-uniform SGPR operands through a constant view.  Persistent:
-// the next tile's loads are issued into VGPRs right after the current tile
-// lands in LDS.  Plus:
-//  * buffer_load_dwordx4 staging through a per-tile buffer descriptor
-//    (32-bit lane offsets, hardware range check returns 0 past the input end,
-//    so the tail needs no per-lane compare) -- fewer VALU ops per load;
-//  * Q0: the shift-0 quantiser above (host selects it when shift & 31 == 0).
-// PROBE (tuning only): 0 = real kernel; 1 = memory path only (no FMA loop);
-// 2 = compute path only (every tile reads the same L2-resident input span);
-// 4 = no staging after the first tile (the tap loop over one LDS image, with
-// the stores); 5 = as 4 without the stores
-// NTL: non-temporal (streaming) input loads; OST: outputs staged through LDS
-// so each store instruction writes whole contiguous lines; NTS: non-temporal
-// output stores; GS: grid-stride tile order (else a contiguous run of tiles
-// per workgroup).
+// at B_t = 2NQ + KPAD + (PR+1) t and the 16 lanes of a ds_read_b128 group hit
+// 16 distinct 16-B bank slots.
+// Memory schedule.  Persistent grid, tiles in grid-stride order (the chip
+// sweeps one contiguous window of the input at a time); the NEXT tile's
+// loads (buffer_load_dwordx4, non-temporal, one descriptor per tile: the
+// range check zero-fills past the end) are issued into VGPRs before this
+// tile's taps and land in LDS after its stores, in one loop iteration, so
+// the wait for them leaves the stores in flight.
+// Taps.  Each lane owns R consecutive outputs and walks the taps as 4
+// polyphase register windows sliding one sample per 4 taps; taps are
+// wave-uniform SGPR pairs issued tap-major through inline asm (pk_fma_tap:
+// every accumulator chain advances one tap before any advances the next).
+// FMA: one v_pk_fma_f32 per tap and output (bit-exact to the -mfma build);
+// strict: R v_pk_mul_f32, then R v_pk_add_f32 (bit-exact to the -O2 build).
+// Tap count.  NT > 0: compiled in (the tap loop unrolls completely).  NT = 0:
+// a.ntaps at run time (<= kCfMaxTaps), the tap loop in chunks of S 4-tap
+// steps whose window groups rotate through S register slots (2S a multiple
+// of PR, so a chunk's LDS reads are one base plus immediates), the chunk's
+// taps loaded one chunk ahead, taps past N skipped (never multiplied by 0:
+// 0 * inf would differ); the LDS image is dynamic, sized by the host.
+// Outputs.  Quantised (Q0: the shift-0 quantiser) and paired across lanes
+// by v_permlane32_swap / v_permlane16_swap (store_wave_lines) so every store
+// instruction writes 1 KiB of whole lines, non-temporal.
 template <bool NTS>
 __device__ __forceinline__ void store16(float4 *p, float4 v) {
     if constexpr (NTS) {
@@ -269,53 +573,74 @@ __device__ __forceinline__ void store_wave_lines(float2 *wo, const float2 (&o)[R
         store16<NTS>((float4 *)(base + LPJ * R * j), make_float4(__uint_as_float(u[j][0]), __uint_as_float(u[j][1]),
                                                                 __uint_as_float(u[j][2]), __uint_as_float(u[j][3])));
 }
-// OST: 0 = each lane stores its own R outputs (two 16-B stores at a 32-B lane
-// stride: every store instruction half-covers its lines); 1 = outputs staged
-// through LDS (two barriers per tile); 2 (R == 4 only) = a v_permlane32_swap
-// per dword pairs lane i's first output pair with lane i+32's and lane i+32's
-// second pair with lane i's, so each of the two store instructions writes
-// 1 KiB of whole lines, with no LDS round trip and no barrier.
-template <int NT, int R, int BLOCK, bool FMA, int MINW, bool Q0, int PROBE = 0, bool NTL = false, int OST = 0,
-          bool NTS = false, bool GS = false, int LAUX = -1, int SAUX = -1, bool ILV = false, int M = 4>
-__global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a) {
-    static_assert(OST != 2 || R == 1 || R == 2 || R == 4 || R == 8, "whole-line stores assume 1, 2, 4 or 8 outputs per lane");
-    static_assert((M * R) % 4 == 0 && M * R <= 16 && (M == 4 || ILV),
-                  "a lane chunk is 4, 8, 12 or 16 input samples; M != 4 takes the ILV tap loop");
-#ifndef SRCDSP_TUNING
-    // the probe / cache-policy / issue-order variants exist for scripts/tune only
-    static_assert(PROBE == 0 && LAUX < 0 && SAUX < 0, "tuning-only variant: build with -DSRCDSP_TUNING");
-#endif
-    constexpr int NQ = (NT + 3) / 4;
+constexpr int kCfMaxTaps = 1024;
+
+// runtime-tap kernel geometry: the window's register slots (the EH + 3 live
+// groups, EH = M(R-1)/4) and the 4-tap steps per chunk (the smallest multiple
+// of the slots that makes 2 U a multiple of the PR granules of a lane chunk,
+// so a chunk's LDS reads are one base plus immediates), and the front slack of
+// its LDS image (granules below the halo that the tail chunk's unconditional
+// window reads may touch)
+__host__ __device__ constexpr int cf32_rt_slots(int M, int R) { return (M * (R - 1)) / 4 + 3; }
+__host__ __device__ constexpr int cf32_rt_steps(int M, int R) {
+    int u = cf32_rt_slots(M, R);
+    while ((2 * u) % (M * R / 2) != 0) u += cf32_rt_slots(M, R);
+    return u;
+}
+__host__ __device__ constexpr int cf32_rt_front(int M, int R) {
+    return 2 * cf32_rt_steps(M, R) + ceildiv(2 * cf32_rt_steps(M, R), M * R / 2) + 2;
+}
+// dynamic LDS granules of the runtime-tap kernel (decim_stream_cf32<0, ...>)
+__host__ __device__ constexpr int cf32_lds_granules(int M, int R, int BLOCK, int ntaps) {
+    return cf32_rt_front(M, R) + (M * BLOCK * R / 2 + 2 * ((ntaps + 3) / 4)) +
+           ((M * BLOCK * R / 2 + 2 * ((ntaps + 3) / 4)) + ceildiv(2 * ((ntaps + 3) / 4), M * R / 2) * (M * R / 2)) /
+               (M * R / 2) +
+           1;
+}
+
+template <int NT, int R, int BLOCK, bool FMA, int MINW, bool Q0, int M>
+__global__ __launch_bounds__(BLOCK, MINW) void decim_stream_cf32(DecimLaunch a) {
+    static_assert((M * R) % 4 == 0 && M * R <= 16, "a lane chunk is 4, 8, 12 or 16 input samples");
+    static_assert(R == 1 || R == 2 || R == 4 || R == 8, "whole-line stores assume 1, 2, 4 or 8 outputs per lane");
+    constexpr bool RT = NT == 0;
+    // the compiled-in tap loop unrolls completely over a window of 4 (NQ + M R / 4)
+    // samples; at M = 4 beyond 128 taps and at M = 1 beyond 64 it no longer stays
+    // in registers (1-2 KiB of scratch per lane), so those lengths take NT = 0
+    static_assert(RT || (M == 1 ? NT <= 64 : (M > 4 || NT <= 128)),
+                  "compile the tap count in only where the unrolled window stays in registers");
+    constexpr int NQC = RT ? (kCfMaxTaps + 3) / 4 : (NT + 3) / 4;  // the register prefetch is sized for this halo
     constexpr int TO = BLOCK * R;
-    constexpr int TG = M * TO / 2 + 2 * NQ;  // staged granules: M TO input samples + the halo
     constexpr int PR = M * R / 2;  // granules per lane chunk (M R samples)
-    constexpr int KPAD = ceildiv(2 * NQ, PR);
-    constexpr int LG = TG + (TG + KPAD * PR) / PR + 1;
-    constexpr int PER = ceildiv(TG, BLOCK);
-    __shared__ float4 lds[LG];
+    constexpr int PER = ceildiv(M * TO / 2 + 2 * NQC, BLOCK);
+    const int N = RT ? a.ntaps : NT;
+    const int NQ = RT ? (N + 3) / 4 : NQC;
+    const int TG = M * TO / 2 + 2 * NQ;  // staged granules: M TO input samples + the halo
+    const int KPAD = ceildiv(2 * NQ, PR);
+    float4 *lds;
+    if constexpr (RT) {
+        extern __shared__ float4 lds_dyn[];
+        lds = lds_dyn + cf32_rt_front(M, R);
+    } else {
+        constexpr int TGC = M * TO / 2 + 2 * NQC, KPC = ceildiv(2 * NQC, PR);
+        __shared__ float4 lds_st[TGC + (TGC + KPC * PR) / PR + 1];
+        lds = lds_st;
+    }
 
     const int ch = blockIdx.y;
     const float2 *in = (const float2 *)a.in + ch * a.in_stride;
     const float2 *hist = (const float2 *)a.hist_in[ch];
     float2 *out = (float2 *)a.out + ch * a.out_stride;
     const long n_in = a.n_in;
-    const int H = NT - 1;
+    const int H = N - 1;
     const int t = threadIdx.x;
     const long nb = gridDim.x;
     const long b = xcd_tile(blockIdx.x, nb);
-    const long per = a.ntiles / nb, rem = a.ntiles % nb;
-    // GS: tiles b, b+nb, b+2nb, ... (the whole grid sweeps one contiguous
-    // window of the input at a time); else a contiguous run of tiles per block
-    const long t_begin = GS ? b : b * per + (b < rem ? b : rem);
-    const long t_end = GS ? a.ntiles : t_begin + per + (b < rem ? 1 : 0);
-    constexpr long kStep1 = 1;
-    const long t_step = GS ? nb : kStep1;
-    if (t_begin == 0 && t_end > 0) write_history(in, n_in, hist, (float2 *)a.hist_out[ch], H);
+    // grid-stride tile order: tiles b, b + nb, b + 2 nb, ...
+    if (b == 0 && a.ntiles > 0) write_history(in, n_in, hist, (float2 *)a.hist_out[ch], H);
 
     float4 v[PER];
     // tiles >= 1: one descriptor per tile, 32-bit lane offsets, range-checked
     auto stage_load = [&](float4 (&v)[PER], long tile) {
-        if constexpr (PROBE >= 2) tile = 1 + (tile & 15);
         const long b0 = M * tile * TO - 4 * NQ;  // >= 0 for tile >= 1
         const long remb = (n_in - b0) * 8;
         const unsigned nrec = (unsigned)(remb > 0xfffffff0L ? 0xfffffff0L : (remb < 0 ? 0 : remb));
@@ -323,19 +648,17 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int g = t + i * BLOCK;
-            if (g < TG) {
-                // aux: bit0 sc0, bit1 nt, bit4 sc1 (LAUX >= 0: tuning override)
+            if ((i + 1) * BLOCK <= M * TO / 2 || g < TG) {  // the tile body always exists; the halo tail may not
                 // lane offset in the VGPR, the per-load step in soffset (an
-                // SGPR constant): one offset VGPR for all PER loads
-                auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * t, 16 * i * BLOCK,
-                                                              LAUX >= 0 ? LAUX : (NTL ? 2 : 0));
+                // SGPR constant): one offset VGPR for all PER loads; aux 2 = nt
+                auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * t, 16 * i * BLOCK, 2);
                 v[i] = make_float4(__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]),
                                    __uint_as_float(w[3]));
             }
         }
     };
-    if (t_begin < t_end) {
-        if (t_begin == 0) {  // tile 0: the halo comes from the history
+    if (b < a.ntiles) {
+        if (b == 0) {  // tile 0: the halo comes from the history
             const long b0 = -4 * NQ;
 #pragma unroll
             for (int i = 0; i < PER; ++i) {
@@ -347,191 +670,222 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_stream2_cf32(DecimLaunch a)
                 }
             }
         } else {
-            stage_load(v, t_begin);
+            stage_load(v, b);
         }
     }
     const int Bt = 2 * NQ + KPAD + (PR + 1) * t;
     // the staged tile lands in LDS once every wave is done with the previous
-    // tile's image (and its output staging, which reuses it)
+    // tile's image
+    // LDS granule of staged granule g = t + i BLOCK: g + (g - 2NQ + KPAD PR) / PR,
+    // the quotient's lane part computed once (BLOCK a multiple of PR)
+    const int lq = (t - 2 * NQ + KPAD * PR) / PR;  // >= 0
     auto stage_to_lds = [&]() {
         SRCDSP_LDS_BARRIER();
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int g = t + i * BLOCK;
-            if (g < TG) lds[g + (g - 2 * NQ + KPAD * PR) / PR] = v[i];
+            if ((i + 1) * BLOCK <= M * TO / 2 || g < TG) {
+                if constexpr (BLOCK % PR == 0)
+                    lds[g + lq + i * (BLOCK / PR)] = v[i];
+                else
+                    lds[g + (g - 2 * NQ + KPAD * PR) / PR] = v[i];
+            }
         }
         SRCDSP_LDS_BARRIER();
     };
-    // one tile: taps over the LDS image, outputs stored.  The loop below
-    // issues the next tile's loads before this and lands them in LDS after
-    // it, all in one iteration: the compiler then waits for the loads with
-    // vmcnt(this tile's stores) and the stores stay in flight.
+    // one tap step (4 taps k = 4q..4q+3) over the R accumulators; xs(r, p) is
+    // sample M r - 4q - p of the lane frame; cp2(j) the tap pair j of the step
+    auto tap_step = [&](f2_t (&acc)[R], int k0, auto first_tag, auto guard_tag, auto &&xs, auto &&cp2, int kn) {
+        constexpr bool FIRST = decltype(first_tag)::value;  // k0 == 0: accumulators start from +0
+        constexpr bool GUARD = decltype(guard_tag)::value;  // taps k0 + p >= kn skipped
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            if (GUARD && k0 + p >= kn) break;
+            const unsigned long long cp = cp2(p >> 1);
+            if constexpr (FMA) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const float2 x = xs(r, p);
+                    const f2_t xv = {x.x, x.y};
+                    if (FIRST && p == 0) pk_fma_tap<false, true>(acc[r], cp, xv);
+                    else if (p & 1) pk_fma_tap<true, false>(acc[r], cp, xv);
+                    else pk_fma_tap<false, false>(acc[r], cp, xv);
+                }
+            } else {
+                f2_t pr[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const float2 x = xs(r, p);
+                    const f2_t xv = {x.x, x.y};
+                    if (p & 1) pk_mul_tap<true>(pr[r], cp, xv);
+                    else pk_mul_tap<false>(pr[r], cp, xv);
+                }
+#pragma unroll
+                for (int r = 0; r < R; ++r) pk_add_acc(acc[r], pr[r]);
+            }
+        }
+    };
+    // one tile: taps over the LDS image, outputs stored
     // WHOLE: the tile's TO outputs all exist (every tile but a partial last one)
     auto do_tile = [&](long tile, auto whole_tag) {
         constexpr bool WHOLE = decltype(whole_tag)::value;
-        ConstPtr<float> tp = const_view<float>(a.coef);
-        asm volatile("" : "+s"(tp));
-        constexpr int GPC = M * R / 4;  // 4-sample groups per lane chunk
-        float2 X[4 * (NQ + GPC)];
-        float yr[R], yi[R];
+        ConstPtr<unsigned long long> tp2 = const_view<unsigned long long>(a.coef);
+        asm volatile("" : "+s"(tp2));
+        f2_t acc[R];
 #pragma unroll
-        for (int r = 0; r < R; ++r) yr[r] = yi[r] = 0.f;
-        auto load_group = [&](int e) {
-            const float4 g0 = lds[Bt + 2 * e + floordiv(2 * e, PR)];
-            const float4 g1 = lds[Bt + 2 * e + 1 + floordiv(2 * e + 1, PR)];
-            X[4 * e + 4 * NQ + 0] = make_float2(g0.x, g0.y);
-            X[4 * e + 4 * NQ + 1] = make_float2(g0.z, g0.w);
-            X[4 * e + 4 * NQ + 2] = make_float2(g1.x, g1.y);
-            X[4 * e + 4 * NQ + 3] = make_float2(g1.z, g1.w);
-        };
+        for (int r = 0; r < R; ++r) acc[r] = f2_t{0.f, 0.f};
+        auto rd = [&](int idx) { return lds[idx]; };
+        if constexpr (!RT) {
+            constexpr int GPC = M * R / 4;  // 4-sample groups per lane chunk
+            float2 X[4 * (NQC + GPC)];
+            auto load_group = [&](int e) {
+                const float4 g0 = rd(Bt + 2 * e + floordiv(2 * e, PR));
+                const float4 g1 = rd(Bt + 2 * e + 1 + floordiv(2 * e + 1, PR));
+                X[4 * e + 4 * NQC + 0] = make_float2(g0.x, g0.y);
+                X[4 * e + 4 * NQC + 1] = make_float2(g0.z, g0.w);
+                X[4 * e + 4 * NQC + 2] = make_float2(g1.x, g1.y);
+                X[4 * e + 4 * NQC + 3] = make_float2(g1.z, g1.w);
+            };
 #pragma unroll
-        for (int e = -1; e < GPC; ++e) load_group(e);
-        if constexpr (PROBE == 1 || PROBE == 3) {
+            for (int e = -1; e < GPC; ++e) load_group(e);
 #pragma unroll
-            for (int r = 0; r < R; ++r) { yr[r] = X[M * r + 4 * NQ].x; yi[r] = X[M * r + 4 * NQ].y; }
-        } else if constexpr (ILV && PROBE != 3) {
-            // tap-major issue order through inline asm: R independent chains
-            // round-robin, taps as SGPR pairs (c[2m], c[2m+1]); FMA: one
-            // pk_fma per tap and output; strict: R products, then R sums
-            ConstPtr<unsigned long long> tp2 = const_view<unsigned long long>(a.coef);
-            asm volatile("" : "+s"(tp2));
-            f2_t acc[R];
-            if constexpr (!FMA) {
-#pragma unroll
-                for (int r = 0; r < R; ++r) acc[r] = f2_t{0.f, 0.f};
-            }
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                if (q + 1 < NQ) load_group(-q - 2);
+            for (int q = 0; q < NQC; ++q) {
+                if (q + 1 < NQC) load_group(-q - 2);
                 if ((q & 3) == 0) asm volatile("" : "+s"(tp2));
+                auto xs = [&](int r, int p) { return X[M * r - 4 * q - p + 4 * NQC]; };
+                auto cp2 = [&](int j) { return tp2[2 * q + j]; };
+                if (q == 0)
+                    tap_step(acc, 4 * q, std::true_type{}, std::integral_constant<bool, (4 * NQC > NT)>{}, xs, cp2, NT);
+                else if (q == NQC - 1)
+                    tap_step(acc, 4 * q, std::false_type{}, std::integral_constant<bool, (4 * NQC > NT)>{}, xs, cp2, NT);
+                else
+                    tap_step(acc, 4 * q, std::false_type{}, std::false_type{}, xs, cp2, NT);
+            }
+        } else {
+            // window groups e (samples 4e..4e+3 of the lane frame) in S rotating
+            // register slots; a step q reads groups -q-1 .. EH-q and prefetches
+            // -q-2; chunks of U steps (q0 a multiple of U)
+            constexpr int EH = (M * (R - 1)) / 4;
+            constexpr int S = cf32_rt_slots(M, R), U = cf32_rt_steps(M, R);
+            static_assert(S == EH + 3 && U % S == 0 && (2 * U) % PR == 0, "window slots / chunk steps");
+            float2 X[S][4];
+            auto slot = [](int e) { return ((e % S) + S) % S; };
+            // chunk base: LDS granule of group c - q0 is cb + 2c + floordiv(2c, PR)
+            auto load_group = [&](int cb, int c) {
+                const float4 g0 = rd(cb + 2 * c + floordiv(2 * c, PR));
+                const float4 g1 = rd(cb + 2 * c + 1 + floordiv(2 * c + 1, PR));
+                float2(&d)[4] = X[slot(c)];
+                d[0] = make_float2(g0.x, g0.y);
+                d[1] = make_float2(g0.z, g0.w);
+                d[2] = make_float2(g1.x, g1.y);
+                d[3] = make_float2(g1.z, g1.w);
+            };
 #pragma unroll
-                for (int p = 0; p < 4; ++p) {
-                    const int k = 4 * q + p;
-                    if (k < NT) {
-                        const unsigned long long cp = tp2[k >> 1];
-                        if constexpr (FMA) {
+            for (int e = -1; e <= EH; ++e) load_group(Bt, e);
+            // the chunk body: U steps from q0 (a multiple of U).  TAIL: the
+            // last chunk, every tap through TapGuarded (k < N, a branch inside
+            // the asm: the compiler sees the same straight line as a full
+            // chunk); its window reads are unconditional (the image has front
+            // slack for the reads past the halo)
+            auto chunk = [&](int q0, auto tail_tag, auto jb_tag, auto je_tag) {
+                constexpr bool TAIL = decltype(tail_tag)::value;
+                constexpr int JB = decltype(jb_tag)::value, JE = decltype(je_tag)::value;  // steps [JB, JE)
+                const int cb = Bt - 2 * q0 - 2 * q0 / PR;
+                ConstPtr<unsigned long long> tc = tp2 + 2 * q0;
+                asm volatile("" : "+s"(tc));
+                const int kb = 4 * q0;
+#pragma unroll
+                for (int j = JB; j < JE; ++j) {
+                    if (j > JB && (j & 3) == 0) asm volatile("" : "+s"(tc));  // taps in batches of 16 (one s_load_dwordx16)
+                    load_group(cb, -j - 2);
+#pragma unroll
+                    for (int p = 0; p < 4; ++p) {
+                        const unsigned long long cp = tc[2 * j + (p >> 1)];
+                        f2_t xv[R];
+#pragma unroll
+                        for (int r = 0; r < R; ++r) {
+                            const int s = M * r - 4 * j - p;  // sample of the frame, relative to -4 q0
+                            const int e = floordiv(s, 4);
+                            const float2 x = X[slot(e)][s - 4 * e];
+                            xv[r] = f2_t{x.x, x.y};
+                        }
+                        if constexpr (TAIL) {
+                            if (p & 1) TapGuarded<R, true, FMA>::run(acc, cp, xv, kb + 4 * j + p, N);
+                            else TapGuarded<R, false, FMA>::run(acc, cp, xv, kb + 4 * j + p, N);
+                        } else if constexpr (FMA) {
 #pragma unroll
                             for (int r = 0; r < R; ++r) {
-                                const float2 x = X[M * r - 4 * q - p + 4 * NQ];
-                                const f2_t xv = {x.x, x.y};
-                                if (k == 0) pk_fma_tap<false, true>(acc[r], cp, xv);
-                                else if (k & 1) pk_fma_tap<true, false>(acc[r], cp, xv);
-                                else pk_fma_tap<false, false>(acc[r], cp, xv);
+                                if (p & 1) pk_fma_tap<true, false>(acc[r], cp, xv[r]);
+                                else pk_fma_tap<false, false>(acc[r], cp, xv[r]);
                             }
                         } else {
                             f2_t pr[R];
 #pragma unroll
                             for (int r = 0; r < R; ++r) {
-                                const float2 x = X[M * r - 4 * q - p + 4 * NQ];
-                                const f2_t xv = {x.x, x.y};
-                                if (k & 1) pk_mul_tap<true>(pr[r], cp, xv);
-                                else pk_mul_tap<false>(pr[r], cp, xv);
+                                if (p & 1) pk_mul_tap<true>(pr[r], cp, xv[r]);
+                                else pk_mul_tap<false>(pr[r], cp, xv[r]);
                             }
 #pragma unroll
                             for (int r = 0; r < R; ++r) pk_add_acc(acc[r], pr[r]);
                         }
                     }
+                    // one step at a time: the next step's group is already in
+                    // flight; hoisting more reads only lengthens the live window
+                    __builtin_amdgcn_sched_barrier(0);
                 }
-            }
-#pragma unroll
-            for (int r = 0; r < R; ++r) { yr[r] = acc[r].x; yi[r] = acc[r].y; }
-        } else
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            if (q + 1 < NQ) load_group(-q - 2);
-            if ((q & 3) == 0) asm volatile("" : "+s"(tp));
-#pragma unroll
-            for (int p = 0; p < 4; ++p) {
-                const int k = 4 * q + p;
-                if (k < NT) {
-                    // PROBE 3 (timing only): compute path with one tap value, no tap loads
-                    const float c = PROBE == 3 ? __builtin_bit_cast(float, a.shift | 0x3c000000u) : tp[k];
-#pragma unroll
-                    for (int r = 0; r < R; ++r) {
-                        const float2 x = X[4 * (r - q) - p + 4 * NQ];
-                        yr[r] = mac<FMA>(c, x.x, yr[r]);
-                        yi[r] = mac<FMA>(c, x.y, yi[r]);
-                    }
-                }
+            };
+            // full chunks while all their taps exist, then the last chunk,
+            // guarded, in two halves: the second only when steps remain there
+            // (the guarded steps' reads and branches are the runtime kernel's
+            // overhead over a compiled tap count)
+            using I0 = std::integral_constant<int, 0>;
+            using IH = std::integral_constant<int, U / 2>;
+            using IU = std::integral_constant<int, U>;
+            int q0 = 0;
+            for (; 4 * (q0 + U) <= N; q0 += U) chunk(q0, std::false_type{}, I0{}, IU{});
+            if (q0 < NQ) {
+                chunk(q0, std::true_type{}, I0{}, IH{});
+                if (q0 + U / 2 < NQ) chunk(q0, std::true_type{}, IH{}, IU{});
             }
         }
         const long n0 = tile * TO + (long)t * R;
         const unsigned sh = a.shift;
         auto q = [&](float y) { return Q0 ? q16f_shift0(y) : q16f(y, sh); };
-        if (PROBE == 5 && a.ntaps != 12345) {  // tuning: no stores
-        } else if constexpr (OST == 2 && WHOLE && R == 2) {  // 16 B per lane: whole lines as they stand
-            store16<NTS>((float4 *)(out + n0), make_float4(q(yr[0]), q(yi[0]), q(yr[1]), q(yi[1])));
-        } else if constexpr (OST == 2 && WHOLE && R == 1) {  // 8 B per lane, lane-contiguous
-            out[n0] = make_float2(q(yr[0]), q(yi[0]));
-        } else if constexpr (OST == 2 && WHOLE) {
+        if constexpr (WHOLE && R == 2) {  // 16 B per lane: whole lines as they stand
+            store16<true>((float4 *)(out + n0), make_float4(q(acc[0].x), q(acc[0].y), q(acc[1].x), q(acc[1].y)));
+        } else if constexpr (WHOLE && R == 1) {  // 8 B per lane, lane-contiguous
+            out[n0] = make_float2(q(acc[0].x), q(acc[0].y));
+        } else if constexpr (WHOLE) {
             float2 o[R];
 #pragma unroll
-            for (int r = 0; r < R; ++r) o[r] = make_float2(q(yr[r]), q(yi[r]));
-            store_wave_lines<R, NTS>(out + tile * TO + (t & ~63) * R, o, t & 63);
-        } else if constexpr (OST == 2) {
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-                if (n0 + r < a.n_out) out[n0 + r] = make_float2(q(yr[r]), q(yi[r]));
-        } else if constexpr (OST == 1) {
-            // outputs -> LDS (reusing the tile image once every wave is done
-            // reading it) -> 16-B lane-contiguous stores of the whole tile
-            const long o0 = tile * TO;
-            SRCDSP_LDS_BARRIER();
-            float2 *ob = (float2 *)lds;
-#pragma unroll
-            for (int r = 0; r < R; ++r) ob[t * R + r] = make_float2(q(yr[r]), q(yi[r]));
-            SRCDSP_LDS_BARRIER();
-            const float4 *ob4 = (const float4 *)lds;
-            if constexpr (WHOLE) {
-#pragma unroll
-                for (int i = 0; i < TO / 2 / BLOCK; ++i) {
-                    const int k = t + i * BLOCK;
-                    if constexpr (SAUX >= 0) {  // tuning override of the store policy
-                        __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
-                            (void *)(out + o0), 0, 0x7ffffff0, 0x00020000);
-                        const float4 v4 = ob4[k];
-                        typedef unsigned u4_t __attribute__((ext_vector_type(4)));
-                        const u4_t u = {__float_as_uint(v4.x), __float_as_uint(v4.y), __float_as_uint(v4.z),
-                                        __float_as_uint(v4.w)};
-                        __builtin_amdgcn_raw_buffer_store_b128(u, ro, 16 * k, 0, SAUX);
-                    } else {
-                        store16<NTS>((float4 *)(out + o0 + 2 * k), ob4[k]);
-                    }
-                }
-            } else {
-                for (int k = t; k < TO; k += BLOCK)
-                    if (o0 + k < a.n_out) out[o0 + k] = ob[k];
-            }
-        } else if (WHOLE && (R % 2) == 0) {
-#pragma unroll
-            for (int r = 0; r < R; r += 2)
-                store16<NTS>((float4 *)(out + n0 + r), make_float4(q(yr[r]), q(yi[r]), q(yr[r + 1]), q(yi[r + 1])));
+            for (int r = 0; r < R; ++r) o[r] = make_float2(q(acc[r].x), q(acc[r].y));
+            store_wave_lines<R, true>(out + tile * TO + (t & ~63) * R, o, t & 63);
         } else {
 #pragma unroll
             for (int r = 0; r < R; ++r)
-                if (n0 + r < a.n_out) out[n0 + r] = make_float2(q(yr[r]), q(yi[r]));
+                if (n0 + r < a.n_out) out[n0 + r] = make_float2(q(acc[r].x), q(acc[r].y));
         }
-        };
+    };
     // Every iteration of the loop prefetches (the workgroup's last tile is
     // peeled off after it), and only the launch's last tile can be partial, so
     // the loop body is one straight path with a fixed number of stores: the
     // compiler waits for the prefetch with a counted vmcnt and the stores stay
     // in flight across iterations.
-    if (t_begin < t_end) {
+    if (b < a.ntiles) {
         stage_to_lds();
-        long tile = t_begin;
-        for (; tile + t_step < t_end; tile += t_step) {
-            if constexpr (PROBE < 4) stage_load(v, tile + t_step);
+        long tile = b;
+        for (; tile + nb < a.ntiles; tile += nb) {
+            stage_load(v, tile + nb);
             do_tile(tile, std::true_type{});
-            if constexpr (PROBE < 4) stage_to_lds();
+            stage_to_lds();
         }
         if ((tile + 1) * TO <= a.n_out)
             do_tile(tile, std::true_type{});
         else
             do_tile(tile, std::false_type{});
     }
-
 }
+
 
 }  // namespace srcdsp
 namespace srcdsp {
@@ -1573,204 +1927,6 @@ __global__ __launch_bounds__(kFirBlock, 4) void fir_stream_f32(DecimLaunch a) {
         else
             do_tile(tile, std::false_type{});
     }
-}
-
-}  // namespace srcdsp
-namespace srcdsp {
-
-// ------------------------------------------------- wave-private cf32 (headline)
-// Persistent complex<float> decimator, M = 4, with NO workgroup barrier: every
-// wave owns wave tiles of 64 lanes x 4 outputs (1024 input samples + the
-// 4*NQ-sample halo) end to end -- loads, LDS image, taps, stores.
-//
-// The wave's LDS image is stored column-major: image granule g (16 B, two
-// samples) = column g/8, row g%8 sits at slot row*NCOL + column.  Column c is
-// lane (c - HC)'s 8-granule chunk (HC halo columns first).  So
-//  * lane t's read of its frame group e (granules 2e, 2e+1 of its chunk) is
-//    slot ((2e)&7)*NCOL + HC + t + floor(2e/8): a per-lane base (16 t) plus a
-//    compile-time immediate, and the 16 lanes of a ds_read_b128 group read 16
-//    consecutive slots -- conflict-free without any pad granules;
-//  * load instruction i, lane l fetches the contiguous image granule 64 i + l
-//    and writes it to slot (l&7)*NCOL + 8i + l/8; with NCOL = 1 (mod 8) the 8
-//    lanes of a ds_write_b128 group land in 8 distinct 16-B bank slots.
-// One image is 8*NCOL*16 B (9,344 B at NQ = 32), so 16 waves fit a CU's LDS
-// with one image each.  A wave lands its prefetched next tile as soon as its
-// own reads of the current image are done (LDS operations of one wave execute
-// in order), so no wave ever waits for another: the four waves of a SIMD
-// drift apart and keep the VALU fed.  The halo (the previous wave tile's
-// tail) is re-read by every wave tile, an L2 hit.
-// Taps: wave-uniform SGPR pairs, issued tap-major (pk_fma_tap) for the FMA
-// contract; the strict contract keeps separately rounded mul/add.
-// PROBE (tuning only): 1 = memory path only (no tap loop); 2 = compute path
-// only (every wave tile loads one of 16 L2-resident spans)
-// 3 = memory path without the halo load; LAUX: load cache policy (2 = nt)
-// SYNC (tuning): one workgroup barrier per wave tile, before its loads issue
-template <int NT, int BLOCK, bool FMA, int MINW, bool Q0, int PROBE = 0, int LAUX = 2, bool SYNC = false>
-__global__ __launch_bounds__(BLOCK, MINW) void decim_wave_cf32(DecimLaunch a) {
-#ifndef SRCDSP_TUNING
-    static_assert(PROBE == 0 && LAUX == 2 && !SYNC, "tuning-only variant: build with -DSRCDSP_TUNING");
-#endif
-    constexpr int R = 4;                      // outputs per lane
-    constexpr int NQ = (NT + 3) / 4;          // 4-tap polyphase groups
-    constexpr int HC = ceildiv(2 * NQ, 8);    // halo columns (8 granules each)
-    constexpr int COLS = 64 + HC;             // loaded columns
-    constexpr int NCOL = COLS + ((1 - COLS % 8) + 8) % 8;  // = 1 (mod 8)
-    constexpr int WG = 8 * COLS;              // image granules (loaded)
-    static_assert(WG % 64 == 0, "whole load instructions per image");
-    constexpr int PER = WG / 64;              // loads per lane
-    constexpr int WPB = BLOCK / 64;
-    constexpr int TO = 64 * R;                // outputs per wave tile
-    constexpr int HALO = 8 * HC * 2;          // halo samples (>= 4 NQ)
-    __shared__ float4 lds[WPB][8 * NCOL];
-
-    const int ch = blockIdx.y;
-    const float2 *in = (const float2 *)a.in + ch * a.in_stride;
-    const float2 *hist = (const float2 *)a.hist_in[ch];
-    float2 *out = (float2 *)a.out + ch * a.out_stride;
-    const long n_in = a.n_in;
-    const int H = NT - 1;
-    const int ln = threadIdx.x & 63;
-    // wave index made wave-uniform for the compiler: tiles, descriptors and
-    // the image base live in SGPRs
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const long nb = gridDim.x;
-    const long b = xcd_tile(blockIdx.x, nb);
-    if (b == 0) write_history(in, n_in, hist, (float2 *)a.hist_out[ch], H);
-    float4 *img = lds[wv];
-    const long step = nb * WPB;
-    long tile = b * WPB + wv;
-
-    float4 v[PER];
-    // image granule 64 i + ln of wave tile `tile` (>= 1): one descriptor per
-    // tile, range-checked (zero past the input end), non-temporal
-    auto stage_load = [&](long tl) {
-        if constexpr (PROBE == 2) tl = 1 + (tl & 15);
-        const long s0 = (long)TO * 4 * tl - HALO;
-        const long remb = (n_in - s0) * 8;
-        const unsigned nrec = (unsigned)(remb > 0xfffffff0L ? 0xfffffff0L : (remb < 0 ? 0 : remb));
-        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)(in + s0), 0, nrec, 0x00020000);
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            if (PROBE == 3 && i == 0) { v[i] = make_float4(0.f, 0.f, 0.f, 0.f); continue; }
-            auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * ln, 1024 * i, LAUX);
-            v[i] = make_float4(__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]),
-                               __uint_as_float(w[3]));
-        }
-    };
-    auto stage_first = [&]() {  // wave tile 0: the halo comes from the history
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const long s = -HALO + 2 * (long)(64 * i + ln);
-            const float2 lo = fetch(in, hist, s, n_in, H), hi = fetch(in, hist, s + 1, n_in, H);
-            v[i] = make_float4(lo.x, lo.y, hi.x, hi.y);
-        }
-    };
-    const int wslot = (ln & 7) * NCOL + (ln >> 3);
-    auto land = [&]() {
-#pragma unroll
-        for (int i = 0; i < PER; ++i) img[wslot + 8 * i] = v[i];
-    };
-    // own frame of lane ln: granule 2e (+1) -> slot ((2e)&7)*NCOL + HC + ln + floor(2e/8)
-    const float4 *rd = img + HC + ln;
-    auto do_tile = [&](long tl, auto whole_tag) {
-        constexpr bool WHOLE = decltype(whole_tag)::value;
-        float2 X[4 * (NQ + R)];
-        auto load_group = [&](int e) {
-            const int o = ((2 * e) & 7) * NCOL + floordiv(2 * e, 8);
-            const float4 g0 = rd[o], g1 = rd[o + NCOL];
-            X[4 * e + 4 * NQ + 0] = make_float2(g0.x, g0.y);
-            X[4 * e + 4 * NQ + 1] = make_float2(g0.z, g0.w);
-            X[4 * e + 4 * NQ + 2] = make_float2(g1.x, g1.y);
-            X[4 * e + 4 * NQ + 3] = make_float2(g1.z, g1.w);
-        };
-#pragma unroll
-        for (int e = -1; e < R; ++e) load_group(e);
-        float yr[R], yi[R];
-        if constexpr (PROBE == 1 || PROBE == 3) {
-#pragma unroll
-            for (int r = 0; r < R; ++r) { yr[r] = X[4 * r + 4 * NQ].x; yi[r] = X[4 * r + 4 * NQ - 4].y; }
-        } else if constexpr (FMA) {
-            ConstPtr<unsigned long long> tp2 = const_view<unsigned long long>(a.coef);
-            asm volatile("" : "+s"(tp2));
-            f2_t acc[R];
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                if (q + 1 < NQ) load_group(-q - 2);
-                if ((q & 3) == 0) asm volatile("" : "+s"(tp2));
-#pragma unroll
-                for (int p = 0; p < 4; ++p) {
-                    const int k = 4 * q + p;
-                    if (k < NT) {
-                        const unsigned long long cp = tp2[k >> 1];
-#pragma unroll
-                        for (int r = 0; r < R; ++r) {
-                            const float2 x = X[4 * (r - q) - p + 4 * NQ];
-                            const f2_t xv = {x.x, x.y};
-                            if (k == 0) pk_fma_tap<false, true>(acc[r], cp, xv);
-                            else if (k & 1) pk_fma_tap<true, false>(acc[r], cp, xv);
-                            else pk_fma_tap<false, false>(acc[r], cp, xv);
-                        }
-                    }
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < R; ++r) { yr[r] = acc[r].x; yi[r] = acc[r].y; }
-        } else {
-            ConstPtr<float> tp = const_view<float>(a.coef);
-            asm volatile("" : "+s"(tp));
-#pragma unroll
-            for (int r = 0; r < R; ++r) yr[r] = yi[r] = 0.f;
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                if (q + 1 < NQ) load_group(-q - 2);
-                if ((q & 3) == 0) asm volatile("" : "+s"(tp));
-#pragma unroll
-                for (int p = 0; p < 4; ++p) {
-                    const int k = 4 * q + p;
-                    if (k < NT) {
-                        const float c = tp[k];
-#pragma unroll
-                        for (int r = 0; r < R; ++r) {
-                            const float2 x = X[4 * (r - q) - p + 4 * NQ];
-                            yr[r] = mac<false>(c, x.x, yr[r]);
-                            yi[r] = mac<false>(c, x.y, yi[r]);
-                        }
-                    }
-                }
-            }
-        }
-        const unsigned sh = a.shift;
-        auto qz = [&](float y) { return Q0 ? q16f_shift0(y) : q16f(y, sh); };
-        const long o0 = tl * TO;
-        if constexpr (WHOLE) {
-            float2 o[R];
-#pragma unroll
-            for (int r = 0; r < R; ++r) o[r] = make_float2(qz(yr[r]), qz(yi[r]));
-            store_wave_lines<R, true>(out + o0, o, ln);
-        } else {
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const long n = o0 + (long)ln * R + r;
-                if (n < a.n_out) out[n] = make_float2(qz(yr[r]), qz(yi[r]));
-            }
-        }
-    };
-    if (tile >= a.ntiles) return;
-    if (tile == 0) stage_first(); else stage_load(tile);
-    // land this tile, issue the next one's loads, then the taps and stores:
-    // the wait for the prefetch (next iteration's land) leaves the stores in
-    // flight; the wave's last tile is peeled so the loop body is straight
-    for (; tile + step < a.ntiles; tile += step) {
-        land();
-        if constexpr (SYNC) __builtin_amdgcn_s_barrier();
-        stage_load(tile + step);
-        do_tile(tile, std::true_type{});
-    }
-    land();
-    if ((tile + 1) * TO <= a.n_out)
-        do_tile(tile, std::true_type{});
-    else
-        do_tile(tile, std::false_type{});
 }
 
 }  // namespace srcdsp

@@ -158,10 +158,26 @@ SRCDSP_API int srcdsp_mixer_destroy(srcdsp_mixer_t h) {
     if (!h) return SRCDSP_OK;
     (void)h->m.order.sync();
     if (h->m.d_table) (void)hipFree(h->m.d_table);
+    if (h->m.d_scratch) (void)hipFree(h->m.d_scratch);
     delete[] h->m.h_table;
     h->m.order.destroy();
     h->m.stage.destroy();
     delete h;
+    return SRCDSP_OK;
+}
+
+SRCDSP_API int srcdsp_mixer_clone(srcdsp_mixer_t h, srcdsp_mixer_t *out) {
+    SRCDSP_ARG_CHECK(h != nullptr && out != nullptr, "mixer_clone: null argument");
+    *out = nullptr;
+    int rc = h->m.order.sync();
+    if (rc) return rc;
+    srcdsp_mixer_t c = nullptr;
+    rc = srcdsp_mixer_create(&c, h->m.N);  // the same table: built from N alone (mixers.h:155-158)
+    if (rc) return rc;
+    c->m.phi = h->m.phi;
+    c->m.freq = h->m.freq;
+    c->m.nominal = h->m.nominal;
+    *out = c;
     return SRCDSP_OK;
 }
 

@@ -7,9 +7,16 @@
 // one batched launch (srcdsp_decim_step_batched) on its own stream.  The only
 // exchange is the optional gather of the decimated outputs, which the caller
 // issues (and times) separately.
+//
+// RCCL is loaded lazily (dlopen at the first srcdsp_comm_create): the
+// single-GPU entries of libsrcdsp_hip.so neither link nor load librccl, and
+// without it srcdsp_comm_create returns SRCDSP_ERR_UNSUPPORTED.  The header
+// gives the types only.
+#include <dlfcn.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -21,6 +28,10 @@ struct srcdsp_comm {
     std::vector<int> devs;
     std::vector<ncclComm_t> comms;
     std::vector<hipStream_t> streams;
+    // the caller's reference plus one per sharded handle built on it: the
+    // communicator is released when the last of them goes, whatever the order
+    // of srcdsp_comm_destroy and srcdsp_decim_sharded_destroy
+    int refs = 1;
 };
 
 struct srcdsp_decim_sharded {
@@ -32,14 +43,68 @@ struct srcdsp_decim_sharded {
 
 namespace {
 
+// the RCCL entry points this file uses, resolved from librccl at run time
+struct Rccl {
+    bool ok = false;
+    std::string why;
+    ncclResult_t (*CommInitAll)(ncclComm_t *, int, const int *) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    const char *(*GetErrorString)(ncclResult_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    ncclResult_t (*Gather)(const void *, void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Send)(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+};
+
+const Rccl &rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void *lib = nullptr;
+        for (const char *name : {"librccl.so.1", "librccl.so"})
+            if ((lib = dlopen(name, RTLD_NOW | RTLD_LOCAL)) != nullptr) break;
+        if (!lib) {
+            r.why = std::string("librccl not loadable: ") + dlerror();
+            return;
+        }
+        auto sym = [&](auto &fn, const char *name) {
+            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(lib, name));
+            return fn != nullptr;
+        };
+        r.ok = sym(r.CommInitAll, "ncclCommInitAll") && sym(r.CommDestroy, "ncclCommDestroy") &&
+               sym(r.GetErrorString, "ncclGetErrorString") && sym(r.GroupStart, "ncclGroupStart") &&
+               sym(r.GroupEnd, "ncclGroupEnd") && sym(r.Gather, "ncclGather") && sym(r.Send, "ncclSend") &&
+               sym(r.Recv, "ncclRecv");
+        if (!r.ok) r.why = "librccl lacks ncclCommInitAll / ncclGather / ncclSend / ncclRecv";
+    });
+    return r;
+}
+
 #define SRCDSP_NCCL_TRY(expr)                                                              \
     do {                                                                                   \
         ncclResult_t _r = (expr);                                                          \
         if (_r != ncclSuccess) {                                                           \
-            ::srcdsp::set_error(std::string(#expr) + ": " + ncclGetErrorString(_r));       \
+            ::srcdsp::set_error(std::string(#expr) + ": " + rccl().GetErrorString(_r));    \
             return SRCDSP_ERR_HIP;                                                         \
         }                                                                                  \
     } while (0)
+
+void comm_release(srcdsp_comm *c) {
+    if (--c->refs > 0) return;
+    int saved = -1;
+    (void)hipGetDevice(&saved);
+    for (size_t r = 0; r < c->devs.size(); ++r) {
+        if (r < c->streams.size() && c->streams[r]) {
+            (void)hipSetDevice(c->devs[r]);
+            (void)hipStreamSynchronize(c->streams[r]);
+            (void)hipStreamDestroy(c->streams[r]);
+        }
+        if (r < c->comms.size() && c->comms[r]) (void)rccl().CommDestroy(c->comms[r]);
+    }
+    if (saved >= 0) (void)hipSetDevice(saved);
+    delete c;
+}
 
 // restores the caller's current device on scope exit
 struct DeviceGuard {
@@ -64,13 +129,18 @@ SRCDSP_API int srcdsp_comm_create(srcdsp_comm_t *out, int ndev, const int *devs)
         SRCDSP_ARG_CHECK(d[r] >= 0 && d[r] < have, "comm_create: device id out of range");
         for (int q = 0; q < r; ++q) SRCDSP_ARG_CHECK(d[q] != d[r], "comm_create: a device listed twice");
     }
+    const Rccl &R = rccl();
+    if (!R.ok) {
+        set_error("comm_create: " + R.why);
+        return SRCDSP_ERR_UNSUPPORTED;
+    }
     DeviceGuard g;
     auto *c = new srcdsp_comm();
     c->devs = d;
     c->comms.assign(ndev, nullptr);
-    ncclResult_t nr = ncclCommInitAll(c->comms.data(), ndev, c->devs.data());
+    ncclResult_t nr = R.CommInitAll(c->comms.data(), ndev, c->devs.data());
     if (nr != ncclSuccess) {
-        set_error(std::string("ncclCommInitAll: ") + ncclGetErrorString(nr));
+        set_error(std::string("ncclCommInitAll: ") + R.GetErrorString(nr));
         delete c;
         return SRCDSP_ERR_HIP;
     }
@@ -90,16 +160,7 @@ SRCDSP_API int srcdsp_comm_create(srcdsp_comm_t *out, int ndev, const int *devs)
 
 SRCDSP_API int srcdsp_comm_destroy(srcdsp_comm_t c) {
     if (!c) return SRCDSP_OK;
-    DeviceGuard g;
-    for (size_t r = 0; r < c->devs.size(); ++r) {
-        if (r < c->streams.size() && c->streams[r]) {
-            (void)hipSetDevice(c->devs[r]);
-            (void)hipStreamSynchronize(c->streams[r]);
-            (void)hipStreamDestroy(c->streams[r]);
-        }
-        if (r < c->comms.size() && c->comms[r]) (void)ncclCommDestroy(c->comms[r]);
-    }
-    delete c;
+    comm_release(c);  // freed now, or with the last sharded handle built on it
     return SRCDSP_OK;
 }
 
@@ -139,6 +200,7 @@ SRCDSP_API int srcdsp_decim_sharded_create(srcdsp_decim_sharded_t *out, srcdsp_c
     DeviceGuard g;
     auto *h = new srcdsp_decim_sharded();
     h->comm = comm;
+    ++comm->refs;
     h->channels = channels;
     h->first.resize(nr);
     h->count.resize(nr);
@@ -174,6 +236,7 @@ SRCDSP_API int srcdsp_decim_sharded_destroy(srcdsp_decim_sharded_t h) {
         (void)hipSetDevice(h->comm->devs[r]);
         for (int k = 0; k < h->count[r]; ++k) srcdsp_decim_destroy(h->handles[h->first[r] + k]);
     }
+    comm_release(h->comm);
     delete h;
     return SRCDSP_OK;
 }
@@ -270,17 +333,17 @@ SRCDSP_API int srcdsp_decim_sharded_gather(srcdsp_decim_sharded_t h, void *const
     const bool even = std::all_of(h->count.begin(), h->count.end(), [&](int k) { return k == h->count[0]; });
     if (even && out_stride == n_out) {
         // every rank's rows are one contiguous block of the same size: ncclGather (rccl.h:745)
-        SRCDSP_NCCL_TRY(ncclGroupStart());
+        SRCDSP_NCCL_TRY(rccl().GroupStart());
         for (int r = 0; r < nr; ++r) {
-            ncclResult_t e = ncclGather(d_out[r], r == root ? d_root : nullptr, (size_t)h->count[r] * row,
-                                        ncclUint8, root, c->comms[r], c->streams[r]);
+            ncclResult_t e = rccl().Gather(d_out[r], r == root ? d_root : nullptr, (size_t)h->count[r] * row,
+                                           ncclUint8, root, c->comms[r], c->streams[r]);
             if (e != ncclSuccess) {
-                (void)ncclGroupEnd();
-                set_error(std::string("ncclGather: ") + ncclGetErrorString(e));
+                (void)rccl().GroupEnd();
+                set_error(std::string("ncclGather: ") + rccl().GetErrorString(e));
                 return SRCDSP_ERR_HIP;
             }
         }
-        SRCDSP_NCCL_TRY(ncclGroupEnd());
+        SRCDSP_NCCL_TRY(rccl().GroupEnd());
         return SRCDSP_OK;
     }
     // uneven partition or strided rows: the root copies its own rows on its
@@ -290,7 +353,7 @@ SRCDSP_API int srcdsp_decim_sharded_gather(srcdsp_decim_sharded_t h, void *const
         SRCDSP_HIP_TRY(hipMemcpy2DAsync((char *)d_root + (size_t)h->first[root] * row, row, d_out[root],
                                         out_stride * ob, row, (size_t)h->count[root], hipMemcpyDeviceToDevice,
                                         c->streams[root]));
-    SRCDSP_NCCL_TRY(ncclGroupStart());
+    SRCDSP_NCCL_TRY(rccl().GroupStart());
     for (int r = 0; r < nr; ++r) {
         if (r == root) continue;
         const bool contiguous = out_stride == n_out;
@@ -299,15 +362,15 @@ SRCDSP_API int srcdsp_decim_sharded_gather(srcdsp_decim_sharded_t h, void *const
         for (int k = 0; k < pieces; ++k) {
             const char *src = (const char *)d_out[r] + (size_t)k * out_stride * ob;
             char *dst = (char *)d_root + ((size_t)h->first[r] + k) * row;
-            ncclResult_t e = ncclSend(src, bytes, ncclUint8, root, c->comms[r], c->streams[r]);
-            if (e == ncclSuccess) e = ncclRecv(dst, bytes, ncclUint8, r, c->comms[root], c->streams[root]);
+            ncclResult_t e = rccl().Send(src, bytes, ncclUint8, root, c->comms[r], c->streams[r]);
+            if (e == ncclSuccess) e = rccl().Recv(dst, bytes, ncclUint8, r, c->comms[root], c->streams[root]);
             if (e != ncclSuccess) {
-                (void)ncclGroupEnd();
-                set_error(std::string("ncclSend/ncclRecv: ") + ncclGetErrorString(e));
+                (void)rccl().GroupEnd();
+                set_error(std::string("ncclSend/ncclRecv: ") + rccl().GetErrorString(e));
                 return SRCDSP_ERR_HIP;
             }
         }
     }
-    SRCDSP_NCCL_TRY(ncclGroupEnd());
+    SRCDSP_NCCL_TRY(rccl().GroupEnd());
     return SRCDSP_OK;
 }

@@ -37,6 +37,7 @@ struct FirCore {
     int init(int kv, unsigned M, const void *coeffs, int ntaps, unsigned flags);
     int set_coeffs(const void *coeffs, int ntaps, bool keep_history);
     int clear_history();
+    int clone_from(FirCore &src);
     void destroy();
     unsigned shift() const { return coeff_scaling - (unsigned)left_shift; }
     int H() const { return ntaps - 1; }
@@ -71,6 +72,11 @@ struct DecimLaunch {
 };
 
 int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, bool mixed);
+// the complex<float> headline kernel (decim_cf32_ct.hip / decim_cf32_rt.hip):
+// with the tap count compiled in (SRCDSP_ERR_UNSUPPORTED for a shape it is not
+// compiled for), or at run time (M in 1/2/3/4/8/16, N <= kCfMaxTaps)
+int launch_cf32_compiled(DecimLaunch L, int channels, unsigned M, int N, bool fma, hipStream_t s);
+int launch_cf32_rt(DecimLaunch L, int channels, unsigned M, bool fma, hipStream_t s);
 
 struct MixerState {
     unsigned N = 4096;
@@ -78,6 +84,10 @@ struct MixerState {
     float nominal = 0.f;
     int16_t *d_table = nullptr;
     int16_t *h_table = nullptr;
+    // grow-only scratch of the unfused mixer -> decimator chain (the mixed
+    // samples between the two launches)
+    void *d_scratch = nullptr;
+    size_t scratch_cap = 0;
     Ordering order;
     HostStage stage;
 };

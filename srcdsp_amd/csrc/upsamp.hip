@@ -12,6 +12,7 @@
 // LDS (c_o[i] = c[o + iL]) and one lane computes the L phases of one input
 // sample from a register copy of its H-sample window.
 #include <algorithm>
+#include <string>
 #include <vector>
 
 #include "ops.h"
@@ -27,6 +28,7 @@ struct srcdsp_up_state {
     int ntaps = 0, H = 0;
     unsigned length = 0;
     int left_shift_factor = 0;
+    std::string h_raw;          // the taps as given (CoefType bytes), for copies
     int32_t *d_coef = nullptr;  // polyphase order: d_coef[o*H + i] = c[o + i*L]
     bool coef_i24 = false;      // every tap in (-2^23, 2^23): v_mad_i32_i24
     bool coef_i16 = false;      // every tap in int16 range: v_dot2 tap pairs (variant 0)
@@ -485,6 +487,7 @@ static int up_set(srcdsp_up_state &u, const void *coeffs, int n) {
     u.H = H;
     u.length = len;
     u.left_shift_factor = (int)std::round(std::log2((double)u.L));  // :119
+    u.h_raw.assign((const char *)coeffs, (size_t)n * (u.variant == UV_CI16_I16 ? 2 : 4));
     return SRCDSP_OK;
 }
 
@@ -636,6 +639,25 @@ SRCDSP_API int srcdsp_up_destroy(srcdsp_up_t h) {
     h->u.order.destroy();
     h->u.stage.destroy();
     delete h;
+    return SRCDSP_OK;
+}
+
+SRCDSP_API int srcdsp_up_clone(srcdsp_up_t h, srcdsp_up_t *out) {
+    SRCDSP_ARG_CHECK(h != nullptr && out != nullptr, "up_clone: null argument");
+    *out = nullptr;
+    srcdsp_up_state &u = h->u;
+    int rc = u.order.sync();
+    if (rc) return rc;
+    srcdsp_up_t c = nullptr;
+    rc = srcdsp_up_create(&c, u.variant, u.L, u.h_raw.data(), u.ntaps);
+    if (rc) return rc;
+    if (hipMemcpy(c->u.d_hist[0], u.d_hist[u.cur], u.hist_cap, hipMemcpyDeviceToDevice) != hipSuccess) {
+        srcdsp_up_destroy(c);
+        set_error("up_clone: history copy failed");
+        return SRCDSP_ERR_HIP;
+    }
+    c->u.cur = 0;
+    *out = c;
     return SRCDSP_OK;
 }
 

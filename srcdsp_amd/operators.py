@@ -99,6 +99,22 @@ def _coeffs(c, kind: str) -> np.ndarray:
 
 class _Handle:
     _destroy = ""
+    _clone = ""  # the C ABI's copy of the object with its state (the reference classes are value types)
+
+    def __copy__(self):
+        """A copy as the reference's implicit copy constructor makes it: the
+        configuration AND the current streaming state (history, phase,
+        registers), so the copy continues the stream like the original."""
+        if not self._clone:
+            raise TypeError(f"{type(self).__name__} is not copyable")
+        c = object.__new__(type(self))
+        c.__dict__.update(self.__dict__)
+        c._h = C.c_void_p()
+        A.call(self._clone, self._h, C.byref(c._h))
+        return c
+
+    def __deepcopy__(self, memo):
+        return self.__copy__()
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -122,6 +138,7 @@ class FilterDnsamplingFir(_Handle):
     float contract ('fma' = sequential FMA chain, 'strict' = mul then add)."""
 
     _destroy = "srcdsp_decim_destroy"
+    _clone = "srcdsp_decim_clone"
 
     def __init__(self, coeffs, M: int = 4, InType="complex<float>", OutType="complex<float>",
                  InternalType="complex<float>", CoefType="float", abs_binding: str = "int", fp: str = "fma"):
@@ -197,6 +214,7 @@ class FilterFir(_Handle):
     """::FilterFir<InType, OutType, InternalType, CoefType> (filters.h:42-169)."""
 
     _destroy = "srcdsp_fir_destroy"
+    _clone = "srcdsp_fir_clone"
 
     def __init__(self, coeffs, InType="complex<float>", OutType="complex<float>", InternalType="complex<float>",
                  CoefType="float", abs_binding: str = "int", fp: str = "fma"):
@@ -243,6 +261,7 @@ class FilterUpsamplingFir(_Handle):
     (upsampling_filters.h:36-326)."""
 
     _destroy = "srcdsp_up_destroy"
+    _clone = "srcdsp_up_clone"
 
     def __init__(self, coeffs, L: int = 4, InType="complex<int16_t>", OutType="complex<int16_t>",
                  InternalType="complex<int32_t>", CoefType="int32_t"):
@@ -300,6 +319,7 @@ class Mixer(_Handle):
     """dsptl::Mixer<complex<int16_t>, complex<int16_t>, int16_t, N> (mixers.h:130-188)."""
 
     _destroy = "srcdsp_mixer_destroy"
+    _clone = "srcdsp_mixer_clone"
 
     def __init__(self, N: int = 4096, InType="complex<int16_t>", OutType="complex<int16_t>", PhaseType="int16_t"):
         if (_kind(InType), _kind(OutType), _kind(PhaseType)) != ("ci16", "ci16", "i16"):
@@ -374,6 +394,7 @@ class FixedPatternCorrelator(_Handle):
     """dsptl::FixedPatternCorrelator<int16_t, int32_t, N, S> (correlators.h:54-316)."""
 
     _destroy = "srcdsp_corr_destroy"
+    _clone = "srcdsp_corr_clone"
 
     def __init__(self, N: int = 32, S: int = 4, InType="int16_t", CompType="int32_t"):
         if (_kind(InType), _kind(CompType)) != ("i16", "i32"):

@@ -180,6 +180,81 @@ int main(int argc, char **argv) {
         dsptl::readBinarySamples(is, back);
         out.put(110, back);
     }
+    // 8. value semantics, as the reference's implicit copies (dnsampling_filters.h:52,
+    //    filters.h:49, upsampling_filters.h:42, correlators.h:85, mixers.h:134):
+    //    copy-initialisation from the coefficient vector, a configured filter copied
+    //    mid-stream continues from the original's history, a bank built as
+    //    std::vector<Filter>(K, proto) (config 3's natural shape), copy assignment
+    {
+        using Dec = dsptl::FilterDnsamplingFir<cf32, cf32, cf32, float, 4>;
+        auto c = as<float>(in[1]);
+        auto x = as<cf32>(in[2]);
+        Dec f = c;  // copy-initialisation: the converting constructor is implicit
+        size_t h = (x.size() / 2) & ~size_t(3);
+        std::vector<cf32> a(x.begin(), x.begin() + h), b(x.begin() + h, x.end());
+        std::vector<cf32> ya(a.size() / 4), yb(b.size() / 4), yc(b.size() / 4);
+        f.step(a, ya);
+        Dec g(f);  // copy after one call: g owns f's history
+        f.step(b, yb);
+        g.step(b, yc);
+        out.put(111, yb);
+        out.put(112, yc);
+        std::vector<Dec> bank(3, g);  // three copies of g's state (after both halves)
+        std::vector<cf32> z(a.size() / 4);
+        const int bank_tags[3] = {113, 123, 124};
+        for (size_t i = 0; i < bank.size(); ++i) {
+            bank[i].step(a, z);
+            out.put(bank_tags[i], z);
+        }
+        Dec k(c);
+        k = f;  // copy assignment: k takes f's state
+        k.step(a, z);
+        out.put(114, z);
+        // the other operators: a copy continues exactly like the original
+        auto cq = as<int32_t>(in[4]);
+        auto xi = as<ci16>(in[3]);
+        std::vector<ci16> xa(xi.begin(), xi.begin() + 1000), xb(xi.begin() + 1000, xi.begin() + 2000);
+        dsptl::Mixer<ci16, ci16, int16_t, 4096> m;
+        m.reset(0.1f);
+        std::vector<ci16> ma(xa.size()), mb(xb.size()), mc(xb.size());
+        m.step(xa, ma);
+        auto m2 = m;
+        m.step(xb, mb);
+        m2.step(xb, mc);
+        out.put(115, mb);
+        out.put(116, mc);
+        FilterFir<ci16, ci16, ci32, int32_t> fi = cq;
+        std::vector<ci16> fa(xa.size()), fb(xb.size()), fc(xb.size());
+        fi.step(xa, fa);
+        auto fi2 = fi;
+        fi.step(xb, fb);
+        fi2.step(xb, fc);
+        out.put(117, fb);
+        out.put(118, fc);
+        auto cu = as<int32_t>(in[7]);
+        dsptl::FilterUpsamplingFir<ci16, ci16, ci32, int32_t, 4> u = cu;
+        std::vector<ci16> ua(4 * xa.size()), ub(4 * xb.size()), uc(4 * xb.size());
+        u.step(xa, ua);
+        auto u2 = u;
+        u.step(xb, ub);
+        u2.step(xb, uc);
+        out.put(119, ub);
+        out.put(120, uc);
+        auto p = as<int32_t>(in[8]);
+        auto xc = as<ci16>(in[9]);
+        dsptl::FixedPatternCorrelator<int16_t, int32_t, 32, 4> corr;
+        std::array<ci32, 32> pat;
+        for (int i = 0; i < 32; ++i) pat[i] = ci32(p[2 * i], p[2 * i + 1]);
+        corr.setPattern(pat);
+        std::vector<ci16> xc1(xc.begin(), xc.begin() + 2000), xc2(xc.begin() + 2000, xc.end());
+        int i1 = -7, i2 = -7;
+        corr.step(xc1, i1);  // no detection in the first part
+        auto corr2 = corr;
+        bool f1 = corr.step(xc2, i1), f2 = corr2.step(xc2, i2);
+        std::vector<int32_t> r = {f1 ? 1 : 0, i1, f2 ? 1 : 0, i2};
+        out.put(121, r);
+        out.put(122, corr2.getRefBitSamples());
+    }
     std::printf("dropin_main: ok\n");
     return 0;
 }

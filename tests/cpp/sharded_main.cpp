@@ -115,6 +115,44 @@ int main(int argc, char **argv) {
     HIP_OK(hipSetDevice(devs[0]));
     HIP_OK(hipMemcpy(all.data(), d_root, all.size() * sizeof(cf32), hipMemcpyDeviceToHost));
     put(out, 200, all.data(), (int64_t)(all.size() * sizeof(cf32)));
+
+    // strided rows (out_stride > n_out): the gather's Memcpy2D / send-recv branch
+    f.reset();
+    const size_t ostr = n_out + 37;
+    std::vector<cf32 *> d_out2(R);
+    for (int r = 0; r < R; ++r) {
+        int first, count;
+        f.partition(r, first, count);
+        HIP_OK(hipSetDevice(devs[r]));
+        HIP_OK(hipMalloc(&d_out2[r], std::max<size_t>(1, count * ostr) * sizeof(cf32)));
+    }
+    f.step(d_in, n, d_out2, ostr, n);
+    HIP_OK(hipSetDevice(devs[0]));
+    HIP_OK(hipMemset(d_root, 0, (size_t)C * n_out * sizeof(cf32)));
+    f.gather(d_out2, ostr, n_out, d_root, 0);
+    comm.synchronize();
+    HIP_OK(hipSetDevice(devs[0]));
+    HIP_OK(hipMemcpy(all.data(), d_root, all.size() * sizeof(cf32), hipMemcpyDeviceToHost));
+    put(out, 201, all.data(), (int64_t)(all.size() * sizeof(cf32)));
+    for (int r = 0; r < R; ++r) {
+        HIP_OK(hipSetDevice(devs[r]));
+        HIP_OK(hipFree(d_out2[r]));
+    }
+
+    // a communicator destroyed before the operator built on it: the operator
+    // keeps its own reference and still steps and gathers
+    {
+        auto *c2 = new dsptl::GpuComm(devs);
+        auto *g2 = new dsptl::ShardedDnsamplingFir<cf32, cf32, cf32, float, 4>(*c2, C, taps);
+        delete c2;
+        g2->step(d_in, n, d_out, n_out, n);
+        g2->gather(d_out, n_out, n_out, d_root, 0);
+        HIP_OK(hipSetDevice(devs[0]));
+        HIP_OK(hipDeviceSynchronize());
+        HIP_OK(hipMemcpy(all.data(), d_root, all.size() * sizeof(cf32), hipMemcpyDeviceToHost));
+        put(out, 202, all.data(), (int64_t)(all.size() * sizeof(cf32)));
+        delete g2;
+    }
     for (int r = 0; r < R; ++r) {
         HIP_OK(hipSetDevice(devs[r]));
         HIP_OK(hipFree((void *)d_in[r]));

@@ -160,6 +160,35 @@ def test_dropin_program_matches_oracle(tmp_path):
     assert np.array_equal(np.frombuffer(got[109], np.float64), np.array(exp))
     # I/Q: whole samples only, output replaced
     assert got[110] == xi.tobytes()
+    # value semantics: copies continue from the original's state, bit-exact
+    h = (len(x) // 2) & ~3
+    d = O.decim(0, 4, c)
+    d.step(x[:h])
+    exp_b = d.step(x[h:])
+    assert got[111] == exp_b.tobytes() and got[112] == exp_b.tobytes()
+    exp_bank = d.step(x[:h])  # the state after both halves, stepped with the first half
+    assert got[113] == exp_bank.tobytes() and got[123] == exp_bank.tobytes() and got[124] == exp_bank.tobytes()
+    assert got[114] == exp_bank.tobytes()
+    mix = O.mixer(4096)
+    mix.reset(0.1)
+    mix.step(xi[:1000])
+    exp_m = mix.step(xi[1000:2000])
+    assert got[115] == exp_m.tobytes() and got[116] == exp_m.tobytes()
+    fo = O.fir(2, cq)
+    fo.step(xi[:1000])
+    exp_f = fo.step(xi[1000:2000])
+    assert got[117] == exp_f.tobytes() and got[118] == exp_f.tobytes()
+    uo = O.up(0, 4, cu)
+    uo.step(xi[:1000])
+    exp_u2 = uo.step(xi[1000:2000])
+    assert got[119] == exp_u2.tobytes() and got[120] == exp_u2.tobytes()
+    co = O.corr(32, 4)
+    co.set_pattern(p)
+    co.step(xc[:2000])
+    f2, i2 = co.step(xc[2000:])
+    r = np.frombuffer(got[121], np.int32)
+    assert f2 and r[0] == 1 and r[2] == 1 and r[1] == i2 and r[3] == i2
+    assert got[122] == co.bit_samples().tobytes()
 
 
 def test_sharded_header_compiles(tmp_path):
@@ -213,3 +242,5 @@ def test_sharded_program_matches_oracle(tmp_path):
         assert got[100 + ch] == exp.tobytes(), ch
         alls.append(O.decim(0, 4, c).step(xs[ch]))
     assert got[200] == np.concatenate(alls).tobytes()
+    assert got[201] == got[200]  # strided rows through the Memcpy2D branch of the gather
+    assert got[202] == got[200]  # operator outliving its GpuComm

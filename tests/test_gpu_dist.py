@@ -1,0 +1,82 @@
+"""The N > 1 code path with the real kernels: two ranks,
+child processes started before they touch the GPU, share cuda:0 and run the
+product's batched decimator on their channels_for_rank share + gather_to_root,
+and the time-split decimator / correlator + first_detection's MIN all-reduce
+(tests/dist_ranks.py; collectives over gloo: two ranks on one GPU cannot form
+an RCCL communicator).  Rank 0's gathered results must equal a
+single-process GPU run byte for byte, and the oracle."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("pat_at", [None, 300000, (1 << 19) - 500, 700000],
+                         ids=["no-hit", "hit-rank0", "hit-straddles", "hit-rank1"])
+def test_two_ranks_on_gpu_match_single_process(tmp_path, pat_at):
+    import torch
+    if torch.cuda.device_count() < 1:  # counts devices without initialising the GPU here
+        pytest.skip("no GPU")
+    out = str(tmp_path / "rank0.npz")
+    port = _free_port()
+    env = dict(os.environ, WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OUT=out,
+               PAT_AT="" if pat_at is None else str(pat_at))
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_ranks.py")],
+                              env=dict(env, RANK=str(r), LOCAL_RANK="0")) for r in range(2)]
+    try:
+        rcs = [p.wait(timeout=180) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert rcs == [0, 0], f"rank exit codes {rcs}"
+    got = np.load(out)
+
+    sys.path.insert(0, HERE)
+    import dist_ranks as R
+    import pyoracle
+    import srcdsp_amd as S
+    from srcdsp_amd.design import hamming_sinc
+    c = hamming_sinc(127)
+    # single process, every channel in one batched launch
+    x = torch.empty((R.CH, R.L), dtype=torch.complex64, device="cuda")
+    for ch in range(R.CH):
+        S.fill_synthetic(x[ch], "cf32", seed=0x5EED, channel=ch)
+    y = torch.empty((R.CH, R.L // 4), dtype=torch.complex64, device="cuda")
+    S.decim_step_batched([S.FilterDnsamplingFir(c, 4) for _ in range(R.CH)], x, y)
+    one = y.cpu().numpy()
+    assert np.array_equal(got["chans"].view(np.uint32), one.view(np.uint32))
+    o = pyoracle.Oracle(1)
+    for ch in (0, R.CH - 1):  # and the oracle on the first and last channel
+        ref = o.decim(0, 4, c).step(o.gen_cf32(0x5EED, ch, 0, R.L))
+        assert np.array_equal(one[ch].view(np.uint32), ref.view(np.uint32))
+    # one long buffer, split in time
+    xs = torch.empty(R.L, dtype=torch.complex64, device="cuda")
+    S.fill_synthetic(xs, "cf32", seed=0x5EED, channel=11)
+    whole = S.FilterDnsamplingFir(c, 4).step(xs).cpu().numpy()
+    assert np.array_equal(got["split"].view(np.uint32), whole.view(np.uint32))
+    p, xc = R.corr_input(pat_at)
+    g = S.FixedPatternCorrelator(R.NC, R.SC)
+    g.setPattern(p)
+    found, idx = g.step(torch.from_numpy(xc).cuda())
+    from srcdsp_amd import dist as D
+    assert int(got["first"]) == (idx if found else D.NO_DETECTION)
+    assert found == (pat_at is not None)
+    go = o.corr(R.NC, R.SC)
+    go.set_pattern(p)
+    ofound, oidx = go.step(xc)
+    assert ofound == found and (not found or oidx == idx)

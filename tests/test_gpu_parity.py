@@ -102,6 +102,37 @@ def test_decim_cf32_any_taps_tile_vs_oracle(S, O, fp, M, ntaps):
         assert np.array_equal(g.step(dev(xs)).cpu().numpy(), r.step(xs)), (off, n)
 
 
+RT_SHAPES = [(4, n) for n in (1, 2, 5, 31, 95, 100, 129, 200, 300, 511, 700, 1024)] + \
+    [(1, n) for n in (1, 31, 100, 300, 1024)] + [(2, n) for n in (3, 95, 200, 513)] + \
+    [(3, n) for n in (4, 50, 301)] + [(8, n) for n in (7, 129, 1000)] + [(16, n) for n in (9, 200, 1023)]
+
+
+@pytest.mark.parametrize("fp", ["fma", "strict"])
+@pytest.mark.parametrize("M,ntaps", RT_SHAPES)
+def test_decim_cf32_runtime_taps_vs_oracle(S, O, fp, M, ntaps):
+    """The headline kernel with the tap count at run time (any N <= 1024 at
+    M in 1/2/3/4/8/16, decim_stream_cf32<0, ...>): full chunks, the guarded
+    last chunk, taps past N never applied (inf / NaN samples in the stream and
+    the history would turn a 0 * x into NaN), tail tiles and chained uneven
+    calls, both float contracts."""
+    rng = np.random.default_rng(M * 7919 + ntaps)
+    c = (rng.standard_normal(ntaps) / max(2, ntaps) ** 0.5).astype(np.float32)
+    x = O[fp].gen_cf32(91 + ntaps, M, 0, 300000, -32768, 32767) + np.float32(0.37)
+    # a few special values, so a tap past N multiplied by one would show
+    for i, v in ((5000, np.inf), (77777, -np.inf), (150001, np.nan), (299990, np.inf)):
+        x[i] = np.complex64(complex(v, 1.0))
+    g = S.FilterDnsamplingFir(c, M, fp=fp) if M > 1 else S.FilterFir(c, "complex<float>", "complex<float>",
+                                                                      "complex<float>", "float", fp=fp)
+    r = O[fp].decim(0, M, c) if M > 1 else O[fp].fir(0, c)
+    for off, n in _chunks(len(x), [65536, M, 8 * M, 70001 * M, 4 * M * 1000 + 8, 3]):
+        n -= n % M
+        if n == 0:
+            continue
+        xs = x[off:off + n]
+        y = g.step(dev(xs)).cpu().numpy()
+        assert np.array_equal(y.view(np.uint32), r.step(xs).view(np.uint32)), (off, n)
+
+
 @pytest.mark.parametrize("kind", ["i16", "i24", "i32", "t16"])
 @pytest.mark.parametrize("M,ntaps", [(2, 1), (2, 33), (2, 127), (4, 17), (4, 63), (4, 200), (8, 16), (8, 255),
                                      (8, 1024), (3, 40), (5, 61), (6, 13), (16, 100)])
@@ -917,3 +948,53 @@ def test_mixer_decimator_correlator_pipeline_device_resident(S, O):
         if exp[0]:
             assert np.array_equal(g.getRefBitSamples(), oc.bit_samples())
     assert sum(h[0] for h in hits) == 1  # the pattern is found once, in the third block
+
+
+# ------------------------------------------------------------ value semantics
+def test_copies_continue_the_stream(S, O):
+    """The reference operators are value types (implicit copy constructors:
+    dnsampling_filters.h:52, filters.h:49, upsampling_filters.h:42,
+    correlators.h:85, mixers.h:134): a copy taken mid-stream (srcdsp_*_clone)
+    continues from the original's history / phase / registers, bit-exact with
+    the original and the oracle."""
+    import copy
+    from srcdsp_amd.design import hamming_sinc, q14, qpsk_pattern
+    o = O["fma"]
+    x = o.gen_cf32(5, 0, 0, 60000)
+    xi = o.gen_ci16(6, 0, 0, 40000, -8192, 8191)
+    c = hamming_sinc(127)
+
+    def check(op, ref, a, b, **kw):
+        y1 = op.step(dev(a), **kw)
+        ref.step(a, **kw)
+        cp = copy.copy(op)
+        ya, yb, yr = op.step(dev(b), **kw).cpu().numpy(), cp.step(dev(b), **kw).cpu().numpy(), ref.step(b, **kw)
+        assert np.array_equal(ya.view(np.uint32), yr.view(np.uint32))
+        assert np.array_equal(yb.view(np.uint32), yr.view(np.uint32))
+        return y1
+
+    check(S.FilterDnsamplingFir(c, 4), o.decim(0, 4, c), x[:30000], x[30000:])
+    check(S.FilterDnsamplingFir(q14(c), 4, "complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int32_t"),
+          o.decim(1, 4, q14(c)), xi[:20000], xi[20000:])
+    check(S.FilterFir(hamming_sinc(31, 0.2)), o.fir(0, hamming_sinc(31, 0.2)), x[:30001], x[30001:])
+    cu = q14(hamming_sinc(32, 0.12) * 4)
+    check(S.FilterUpsamplingFir(cu, 4), o.up(0, 4, cu), xi[:5000], xi[5000:9000])
+    m = S.Mixer(4096)
+    m.reset(0.1)
+    mo = o.mixer(4096)
+    mo.reset(0.1)
+    check(m, mo, xi[:17], xi[17:30000])
+    # correlator: registers and history carried into the copy (detection in the second part)
+    p = qpsk_pattern(32, 500, seed=3)
+    xc = np.random.default_rng(8).integers(-125, 126, size=(8000, 2)).astype(np.int32)
+    for k in range(32):
+        xc[5000 + 4 * k] += 2 * p[k]
+    xc = xc.astype(np.int16)
+    g = S.FixedPatternCorrelator(32, 4)
+    g.setPattern(p)
+    go = o.corr(32, 4)
+    go.set_pattern(p)
+    assert not g.step(dev(xc[:4000]))[0] and not go.step(xc[:4000])[0]
+    g2 = copy.copy(g)
+    r1, r2, rr = g.step(dev(xc[4000:])), g2.step(dev(xc[4000:])), go.step(xc[4000:])
+    assert r1 == r2 == rr and rr[0]
