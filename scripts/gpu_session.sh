@@ -13,7 +13,8 @@
 #   ramp             cold ramps of tune variants ${VARIANTS} (scripts/tune/ramp.py), IDLE s apart
 #   envelope         scripts/shape_envelope.py ${ENV_M}
 #   census           workgroup placement census (scripts/tune/census.py)
-#   clock            in-kernel clock of a tune variant over a cold start (ramp.py, ${CLOCK_VARIANTS})
+#   ab               same-box A/B of scripts/tune/ab/libsrcdsp_hip_base.so vs the tree's library
+#                    (scripts/tune/ab_libs.sh; WORKLOADS, ROUNDS, LAUNCHES)
 #   dist             the 2-rank GPU test of the N > 1 path (tests/test_gpu_dist.py)
 #   cpp              the drop-in C++ tests (tests/test_dropin_cpp.py -m gpu)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -52,6 +53,7 @@ for s in ${STEPS:-smoke tests bench}; do
       done ;;
     envelope) step envelope_$TAG 600 python -u scripts/shape_envelope.py ${ENV_M} ;;
     census) step census_$TAG 120 python -u scripts/tune/census.py ;;
+    ab) step ab_$TAG 1000 bash scripts/tune/ab_libs.sh ;;
     dist) step dist_$TAG 300 python -u -m pytest tests/test_gpu_dist.py -m gpu -v --timeout 240 --timeout-method thread ;;
     cpp) step cpp_$TAG 600 python -u -m pytest tests/test_dropin_cpp.py -m gpu -v --timeout 240 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;

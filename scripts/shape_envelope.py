@@ -17,8 +17,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import srcdsp_amd as S  # noqa: E402
 from srcdsp_amd.design import hamming_sinc  # noqa: E402
 
-COMPILED = {4: (63, 64, 127, 128, 255, 256), 8: (127, 128, 255, 256), 16: (127, 128, 255, 256),
-            2: (63, 64, 127, 128), 3: (63, 64, 127, 128), 1: (63, 64, 127, 128)}
+COMPILED = {4: (63, 64, 127, 128), 8: (127, 128, 255, 256), 16: (127, 128, 255, 256),
+            2: (63, 64, 127, 128), 3: (63, 64, 127, 128), 1: (63, 64)}
 SHAPES = {4: (31, 63, 95, 100, 126, 127, 129, 200, 255, 300, 511, 1024),
           1: (31, 62, 63, 100, 127, 129, 255, 300),
           2: (62, 63, 95, 127, 129, 200),
