@@ -5,10 +5,10 @@ Default workload = BASELINE.json configs[1] (the headline metric): the 127-tap
 complex<float> decimate-by-4 FilterDnsamplingFir over 2^28 device-resident
 synthetic samples, one step() per timed step (one kernel launch), FMA float
 contract.  With --gpus N (launched by torch.distributed.run) every rank owns
-8 channels (default at N>1; --channels-per-gpu) -- configs[2]'s 64 channels
-over 8 GPUs, one batched launch per step per rank, weak scaling, no
-collective in the timed region; the RCCL result gather to rank 0 is timed
-separately (gather_ms).
+the same work as N = 1 (one 2^28-sample channel; --channels-per-gpu 8 at N = 8
+gives configs[2]'s 64 channels over 8 GPUs, one batched launch per step per
+rank): weak scaling, no collective in the timed region; the RCCL result gather
+to rank 0 is timed separately (gather_ms).
 
 Other workloads (--workload): mixdecim (config 4, mixer -> fixed-point
 decimator, fused), corr (config 5, 1024-lag correlator), fir (config 1 shape on
@@ -50,9 +50,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=100)
     p.add_argument("--workload", default="decim", choices=["decim", "mixdecim", "ci16decim", "corr", "fir", "up", "fifo", "iq"])
     p.add_argument("--samples", type=int, default=1 << 28, help="input samples per channel per step")
-    # default: 1 channel at N=1 (configs[1], the headline); 8 per GPU at N>1,
-    # i.e. configs[2]'s 64 independent channels over 8 GPUs, weak-scaled
-    p.add_argument("--channels-per-gpu", type=int, default=None)
+    # default 1 channel per GPU at every N (configs[1]'s work on each rank, so
+    # per-GPU work is fixed as N grows); 8 at N = 8 is configs[2]'s 64 channels
+    p.add_argument("--channels-per-gpu", type=int, default=1)
     p.add_argument("--fp", default="fma", choices=["fma", "strict"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=1 << 27, help="samples timed on the reference CPU path")
@@ -653,8 +653,8 @@ def main():
     from srcdsp_amd.dist import gather_to_root, max_over_ranks
     S.lib()  # loud failure if the HIP library is missing
     L = args.samples - args.samples % 4
-    if args.channels_per_gpu is None:
-        args.channels_per_gpu = 1 if world == 1 or args.workload != "decim" else 8
+    if args.workload != "decim":
+        args.channels_per_gpu = 1
     work = WORKLOADS[args.workload](S, torch, L, args.channels_per_gpu, rank, args.fp)
     stream = torch.cuda.current_stream()
 

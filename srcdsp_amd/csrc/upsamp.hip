@@ -249,7 +249,38 @@ __global__ __launch_bounds__(kUpBlockD, MINW) void up_tile_dot2(const uint32_t *
     uint32_t *pl = (uint32_t *)ug;
     const int PDW = 4 * PGR;  // dwords per plane
     const int ng = 2 * PGR;
-    for (int g = t; g < ng; g += kUpBlockD) {
+    auto lo = [](uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x05040100u); };
+    auto hi = [](uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x07060302u); };
+    auto put = [&](int g, const uint32_t (&w)[5]) {
+        *(uint2 *)&pl[0 * PDW + 2 * g] = make_uint2(lo(w[0], w[1]), lo(w[2], w[3]));
+        *(uint2 *)&pl[1 * PDW + 2 * g] = make_uint2(hi(w[0], w[1]), hi(w[2], w[3]));
+        *(uint2 *)&pl[2 * PDW + 2 * g] = make_uint2(lo(w[1], w[2]), lo(w[3], w[4]));
+        *(uint2 *)&pl[3 * PDW + 2 * g] = make_uint2(hi(w[1], w[2]), hi(w[3], w[4]));
+    };
+    // a tile whose whole span (halo included) lies inside the input: the
+    // lane's first three granules are loaded together, then written (one
+    // exposed load latency per tile instead of one per granule)
+    constexpr int NI = 3;
+    const bool interior = j0 - 8L * HG >= 0 && j0 + TI + 1 <= n_in;
+    int g1 = t;  // first granule of the generic loop
+    if (interior) {
+        uint32_t w[NI][5];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int g = t + i * kUpBlockD;
+            if (i < 2 || g < ng) {  // ng >= 2 * kUpBlockD
+                const long s0 = j0 - 8L * HG + 4L * g;
+                const uint4 v = *(const uint4 *)(in + s0);
+                w[i][0] = v.x; w[i][1] = v.y; w[i][2] = v.z; w[i][3] = v.w;
+                w[i][4] = in[s0 + 4];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+            if (i < 2 || t + i * kUpBlockD < ng) put(t + i * kUpBlockD, w[i]);
+        g1 = t + NI * kUpBlockD;
+    }
+    for (int g = g1; g < ng; g += kUpBlockD) {
         const long s0 = j0 - 8L * HG + 4L * g;
         uint32_t w[5];
         if (s0 >= 0 && s0 + 5 <= n_in) {
@@ -260,12 +291,7 @@ __global__ __launch_bounds__(kUpBlockD, MINW) void up_tile_dot2(const uint32_t *
 #pragma unroll
             for (int k = 0; k < 5; ++k) w[k] = up_fetch<UV_CI16_I32>(in, hist_in, s0 + k, n_in, Hm1);
         }
-        auto lo = [](uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x05040100u); };
-        auto hi = [](uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x07060302u); };
-        *(uint2 *)&pl[0 * PDW + 2 * g] = make_uint2(lo(w[0], w[1]), lo(w[2], w[3]));
-        *(uint2 *)&pl[1 * PDW + 2 * g] = make_uint2(hi(w[0], w[1]), hi(w[2], w[3]));
-        *(uint2 *)&pl[2 * PDW + 2 * g] = make_uint2(lo(w[1], w[2]), lo(w[3], w[4]));
-        *(uint2 *)&pl[3 * PDW + 2 * g] = make_uint2(hi(w[1], w[2]), hi(w[3], w[4]));
+        put(g, w);
     }
     __syncthreads();
     // lane base: input j0 + 8t = plane dword D0 = 4t + 4*HG (granule gb).  Input
@@ -380,6 +406,10 @@ __global__ __launch_bounds__(kUpBlockD, MINW) void up_tile_dot2(const uint32_t *
     // conflict-free) -> whole-line 16-B stores of the tile's contiguous output
     constexpr int GPLo = R * LR / 4;    // output granules per lane
     constexpr int STR = GPLo + 1;       // padded lane stride (odd)
+    // (each lane storing its own 128-B output line directly, 8 x 16 B at a
+    // 128-B lane stride, measured 30 % slower with plain stores and 5.5x
+    // slower with nt stores than this LDS transpose into whole-line stores:
+    // profiles/tuning/r03_up_stage_ab.txt)
     __syncthreads();                    // every wave is done reading the planes
     uint4 *ob = ug;
 #pragma unroll
@@ -395,30 +425,36 @@ __global__ __launch_bounds__(kUpBlockD, MINW) void up_tile_dot2(const uint32_t *
     __syncthreads();
     const long wbase = (long)LR * j0;             // first output word of the tile
     const long wend = (long)LR * n_total;         // output words of the call
+    // one whole ds_read_b128 per granule (volatile: the compiler split these
+    // reads into ds_read_b32 / ds_read2_b32 for the partial-tile branch, whose
+    // 32-lane groups at a 16-B stride hit 8 banks: 25 M conflict cycles per
+    // launch at L = 4, 2^26 inputs)
+    typedef uint32_t o4v_t __attribute__((ext_vector_type(4)));
+    typedef const volatile __attribute__((address_space(3))) o4v_t *lds_o4v;
+    auto oread = [&](int G) { return *(lds_o4v)(&ob[(G / GPLo) * STR + (G % GPLo)]); };
+    if (wbase + 4L * GPLo * kUpBlockD <= wend) {
+        // whole tile: every granule read, then every store issued, at one
+        // base address (no per-store range checks)
+        o4v_t v[GPLo];
 #pragma unroll
-    for (int i = 0; i < GPLo; ++i) {
-        const int G = i * kUpBlockD + t;          // output granule within the tile
-        // one whole ds_read_b128 (volatile: the compiler split this read into
-        // ds_read_b32 / ds_read2_b32 for the partial-tile branch below, whose
-        // 32-lane groups at a 16-B stride hit 8 banks: 25 M conflict cycles
-        // per launch at L = 4, 2^26 inputs)
-        typedef uint32_t o4v_t __attribute__((ext_vector_type(4)));
-        typedef const volatile __attribute__((address_space(3))) o4v_t *lds_o4v;
-        const o4v_t vv4 = *(lds_o4v)(&ob[(G / GPLo) * STR + (G % GPLo)]);
-        const uint4 v = make_uint4(vv4[0], vv4[1], vv4[2], vv4[3]);
-        const long w0 = wbase + 4L * G;
-        if (w0 + 4 <= wend) {
+        for (int i = 0; i < GPLo; ++i) v[i] = oread(i * kUpBlockD + t);
+        uint32_t *o = out + wbase + 4L * t;
+#pragma unroll
+        for (int i = 0; i < GPLo; ++i) {
             if constexpr (NTS) {  // streaming store: the output is written once, 4L x the input bytes
-                typedef unsigned u4_t __attribute__((ext_vector_type(4)));
-                __builtin_nontemporal_store((u4_t){v.x, v.y, v.z, v.w}, (u4_t *)(out + w0));
+                __builtin_nontemporal_store(v[i], (o4v_t *)(o + 4 * i * kUpBlockD));
             } else {
-                *(uint4 *)(out + w0) = v;
+                *(o4v_t *)(o + 4 * i * kUpBlockD) = v[i];
             }
-        } else {
-            const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
-            for (int u = 0; u < 4; ++u)
-                if (w0 + u < wend) out[w0 + u] = vv[u];
         }
+        return;
+    }
+    for (int i = 0; i < GPLo; ++i) {  // the call's last, partial tile
+        const int G = i * kUpBlockD + t;          // output granule within the tile
+        const o4v_t vv4 = oread(G);
+        const long w0 = wbase + 4L * G;
+        for (int u = 0; u < 4; ++u)
+            if (w0 + u < wend) out[w0 + u] = vv4[u];
     }
 }
 
