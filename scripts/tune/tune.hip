@@ -164,6 +164,11 @@ extern "C" int tune_decim(int variant, int grid, const float *d_coef, const void
     case 202: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 2, true, 0, true, 2, true, true, -1, -1, true>, grid, 512, L, s);
     case 203: L.ntiles = tiles(256 * 4); return launch(decim_stream2_cf32_tune<127, 4, 256, true, 4, true, 0, true, 2, true, true, -1, -1, true>, grid, 256, L, s);
     case 204: L.ntiles = tiles(256 * 8); return launch(decim_stream2_cf32_tune<127, 8, 256, true, 2, true, 0, true, 2, true, true, -1, -1, true>, grid, 256, L, s);
+    case 610: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 0, true, 2, true, true, 0, -1, true>, grid, 512, L, s);  // ILV, load aux 0
+    case 611: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 0, true, 2, true, true, 1, -1, true>, grid, 512, L, s);  // ILV, load aux 1
+    case 612: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 0, true, 2, true, true, 3, -1, true>, grid, 512, L, s);  // ILV, load aux 3
+    case 613: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 0, true, 2, true, true, 16, -1, true>, grid, 512, L, s);  // ILV, load aux 16
+    case 614: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 0, true, 2, true, true, 18, -1, true>, grid, 512, L, s);  // ILV, load aux 18
     case 70: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 0, true, 2, true, true>, grid, 512, L, s);
     case 71: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 4, true, 1, true, 2, true, true>, grid, 512, L, s);
     case 72: L.ntiles = tiles(512 * 4); return launch(decim_stream2_cf32_tune<127, 4, 512, true, 2, true, 0, true, 2, true, true>, grid, 512, L, s);
