@@ -9,7 +9,7 @@
 #   bench            bench.py ${BENCH_ARGS} (default: the headline, driver protocol --steps 20 --warmup 5)
 #   bench_all        every workload's bench line (steady protocol)
 #   prof             rocprofv3 --kernel-trace --stats of bench.py ${BENCH_ARGS} (per-dispatch CSV kept)
-#   pmc              FETCH_SIZE / WRITE_SIZE passes (scripts/pmc_traffic.py ${PMC_ARGS})
+#   pmc              FETCH_SIZE / WRITE_SIZE passes (scripts/pmc_traffic.py) for each of ${PMC_WORKLOADS}
 #   ramp             cold ramps of tune variants ${VARIANTS} (scripts/tune/ramp.py), IDLE s apart
 #   envelope         scripts/shape_envelope.py ${ENV_M}
 #   census           workgroup placement census (scripts/tune/census.py)
@@ -43,7 +43,10 @@ for s in ${STEPS:-smoke tests bench}; do
       done ;;
     prof) step prof_$TAG 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv \
             -- python3 bench.py --no-cpu-baseline --no-pcie ${BENCH_ARGS:---steps 20 --warmup 5} ;;
-    pmc) step pmc_$TAG 600 python -u scripts/pmc_traffic.py ${PMC_ARGS} ;;
+    pmc)
+      for w in ${PMC_WORKLOADS:-decim}; do
+        step pmc_${w}_$TAG 600 python -u scripts/pmc_traffic.py --workload $w --tag $TAG
+      done ;;
     ramp)
       : > gpurun_out/ramp_$TAG.jsonl
       for v in ${VARIANTS:-prod}; do
