@@ -49,7 +49,8 @@ def parse():
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=100)
     p.add_argument("--workload", default="decim", choices=["decim", "mixdecim", "ci16decim", "corr", "fir", "up", "fifo", "iq"])
-    p.add_argument("--samples", type=int, default=1 << 28, help="input samples per channel per step")
+    p.add_argument("--samples", type=int, default=None,
+                   help="input samples per channel per step (default 2^28; corr: 2^26, config 5's 64 Msamp)")
     # default 1 channel per GPU at every N (configs[1]'s work on each rank, so
     # per-GPU work is fixed as N grows); 8 at N = 8 is configs[2]'s 64 channels
     p.add_argument("--channels-per-gpu", type=int, default=1)
@@ -652,6 +653,8 @@ def main():
     import srcdsp_amd as S
     from srcdsp_amd.dist import gather_to_root, max_over_ranks
     S.lib()  # loud failure if the HIP library is missing
+    if args.samples is None:
+        args.samples = (1 << 26) if args.workload == "corr" else (1 << 28)
     L = args.samples - args.samples % 4
     if args.workload != "decim":
         args.channels_per_gpu = 1
