@@ -17,7 +17,9 @@
 
 #include <algorithm>
 #include <mutex>
+#include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "ops.h"
