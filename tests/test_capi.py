@@ -68,3 +68,14 @@ def test_argument_errors_need_no_gpu(capi):
     assert lib.srcdsp_decim_step(None, None, 0, None, 0, None) == capi.ERR_ARG
     assert lib.srcdsp_mixer_create(C.byref(h), 2) == capi.ERR_ARG
     assert lib.srcdsp_fill_synthetic(None, 0, 5, 0, 0, 0, 0, 1, None) == capi.ERR_ARG
+
+
+def test_library_does_not_link_rccl(capi):
+    """RCCL is dlopened by srcdsp_comm_create only (multi.hip), so single-GPU
+    users neither link nor load it: no DT_NEEDED entry for librccl."""
+    import subprocess
+    out = subprocess.run(["readelf", "-d", capi.LIB_PATH], capture_output=True, text=True)
+    if out.returncode != 0:
+        pytest.skip("readelf unavailable")
+    needed = re.findall(r"\(NEEDED\)\s+Shared library: \[([^\]]+)\]", out.stdout)
+    assert needed and not [n for n in needed if "rccl" in n], needed
