@@ -631,6 +631,80 @@ def test_config4_size_properties(S, O):
     torch.cuda.empty_cache()
 
 
+def test_decim_cf32_beyond_4gib_one_channel(S, O):
+    """One channel past 4 GiB: 2^30 + a ragged tail of complex<float> samples
+    (8 GiB in, one step()), so byte offsets pass 2^32 and sample indices 2^29:
+    spot windows around the 4 GiB boundary, random interior, the ragged last
+    tile, and the history left for the next call, against the oracle on the
+    same input windows."""
+    import torch
+    from srcdsp_amd.design import hamming_sinc
+    c = hamming_sinc(127)
+    L = (1 << 30) + 4 * 1237
+    x = torch.empty(L, dtype=torch.complex64, device="cuda")
+    S.fill_synthetic(x, "cf32", seed=0x5EED, channel=5)
+    f = S.FilterDnsamplingFir(c, 4, fp="fma")
+    y = torch.empty(L // 4, dtype=torch.complex64, device="cuda")
+    f.step(x, y)
+    torch.cuda.synchronize()
+    n_out = L // 4
+    b4 = (1 << 29) // 4  # the output whose inputs straddle byte offset 2^32
+    rng = np.random.default_rng(6)
+    for s0 in [0, b4 - 40, b4 - 1, b4 + 7, n_out - 64, *map(int, rng.integers(40, n_out - 64, 4))]:
+        lo = max(0, 4 * s0 - 128)
+        xin = x[lo:4 * (s0 + 64)].cpu().numpy()
+        assert np.array_equal(xin, O["fma"].gen_cf32(0x5EED, 5, lo, len(xin))), s0
+        r = O["fma"].decim(0, 4, c).step(xin)[(4 * s0 - lo) // 4:]
+        got = y[s0:s0 + 64].cpu().numpy()
+        assert np.array_equal(got, r[:len(got)]), s0
+    assert f.state()["history"].tobytes() == x[L - 126:].cpu().numpy().tobytes()
+    del x, y
+    torch.cuda.empty_cache()
+
+
+def test_mixdecim_beyond_2p31_samples(S, O):
+    """Config 4's fused chain on one call of 2^31 + a ragged tail of
+    complex<int16_t> samples (8 GiB in): sample indices pass 2^31, so the
+    NCO phase (phi0 + k*freq) mod N and every tile offset must be 64-bit.
+    Output windows before and after sample 2^31 and at the end against the
+    reference mixer -> decimator pair on the same input windows (the oracle
+    mixer advanced by stepping zeros: the phase does not depend on the data)."""
+    import torch
+    from srcdsp_amd.design import hamming_sinc, q14
+    cq = q14(hamming_sinc(127))
+    L = (1 << 31) + 4 * 2048 * 3 + 4 * 77
+    x = torch.empty((L, 2), dtype=torch.int16, device="cuda")
+    S.fill_synthetic(x, "ci16", seed=0x5EED, channel=3, lo=-8192, hi=8191)
+    m = S.Mixer(4096)
+    m.reset(0.1)
+    d = S.FilterDnsamplingFir(cq, 4, "complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int32_t")
+    y = S.MixerDecimatorChain(m, d).step(x)
+    torch.cuda.synchronize()
+    om = O["strict"].mixer(4096)
+    om.reset(0.1)
+    n_out = L // 4
+    b31 = (1 << 31) // 4
+    starts = [0, 2048 - 3, b31 - 100, b31 + 5, n_out - 64]
+    zeros = np.zeros((1 << 24, 2), np.int16)
+    pos = 0
+    for s0 in starts:
+        lo = max(0, 4 * s0 - 128)
+        hi = 4 * (s0 + 64)
+        while pos < lo:
+            k = min(lo - pos, len(zeros))
+            om.step(zeros[:k])
+            pos += k
+        xin = x[lo:hi].cpu().numpy()
+        assert np.array_equal(xin, O["strict"].gen_ci16(0x5EED, 3, lo, hi - lo, -8192, 8191)), s0
+        mixed = om.step(xin)
+        pos = hi
+        r = O["strict"].decim(1, 4, cq).step(mixed)[(4 * s0 - lo) // 4:]
+        got = y[s0:s0 + 64].cpu().numpy()
+        assert np.array_equal(got, r[:len(got)]), s0
+    del x, y
+    torch.cuda.empty_cache()
+
+
 def test_fir_and_up_bench_size_properties(S, O):
     """The fir and up bench workloads at their full sizes (2^28 float samples
     through the 31-tap FilterFir<float,cf32,float,float>; 2^26 ci16 inputs
