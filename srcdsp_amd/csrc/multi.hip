@@ -16,6 +16,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -32,8 +33,9 @@ struct srcdsp_comm {
     std::vector<hipStream_t> streams;
     // the caller's reference plus one per sharded handle built on it: the
     // communicator is released when the last of them goes, whatever the order
-    // of srcdsp_comm_destroy and srcdsp_decim_sharded_destroy
-    int refs = 1;
+    // of srcdsp_comm_destroy and srcdsp_decim_sharded_destroy (atomic: handles
+    // built on one comm may be destroyed from different threads)
+    std::atomic<int> refs{1};
 };
 
 struct srcdsp_decim_sharded {
@@ -93,7 +95,7 @@ const Rccl &rccl() {
     } while (0)
 
 void comm_release(srcdsp_comm *c) {
-    if (--c->refs > 0) return;
+    if (c->refs.fetch_sub(1) > 1) return;
     int saved = -1;
     (void)hipGetDevice(&saved);
     for (size_t r = 0; r < c->devs.size(); ++r) {
@@ -202,7 +204,7 @@ SRCDSP_API int srcdsp_decim_sharded_create(srcdsp_decim_sharded_t *out, srcdsp_c
     DeviceGuard g;
     auto *h = new srcdsp_decim_sharded();
     h->comm = comm;
-    ++comm->refs;
+    comm->refs.fetch_add(1);
     h->channels = channels;
     h->first.resize(nr);
     h->count.resize(nr);
