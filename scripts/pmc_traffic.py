@@ -65,6 +65,7 @@ def main():
     ap.add_argument("--channels", type=int, default=1, help="decim only: channels per launch (config 3's share: 8)")
     a = ap.parse_args()
     key = KERNEL_KEYS[a.workload]
+    steps_run = 6  # bench.py --warmup 1 --steps 5: every step's dispatches are counted
     bench_args = ["--workload", a.workload, "--steps", "5", "--warmup", "1", "--no-cpu-baseline", "--no-pcie",
                   "--samples", str(a.samples)]
     if a.channels > 1:
@@ -75,10 +76,12 @@ def main():
         rows = [v for (n, d), v in per.items() if key in n]
         if not rows:
             raise RuntimeError(f"kernel {key} not found among {sorted({n for n, _ in per})}")
+        # per step: a step may be several dispatches (the batched complex<float>
+        # decimator launches once per channel)
         for c in counters:
-            vals = [r[c] for r in rows if c in r]
-            res[c] = sum(vals) / len(vals)
+            res[c] = sum(r[c] for r in rows if c in r) / steps_run
         res["dispatches"] = len(rows)
+        res["dispatches_per_step"] = len(rows) / steps_run
     L = (a.samples - a.samples % 4) * a.channels
     if a.workload == "up":
         L //= 4  # bench.py's up workload takes samples/4 inputs (4x as many outputs)

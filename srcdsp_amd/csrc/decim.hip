@@ -220,8 +220,20 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
         // BASELINE lengths (127/128: configs 2 and 3) and the common neighbouring
         // power-of-two lengths; any other N <= 1024 takes the same kernel with
         // the tap count at run time
-        rc = launch_cf32_compiled(L, channels, f.M, f.ntaps, fma, s);
-        if (rc == SRCDSP_ERR_UNSUPPORTED) rc = launch_cf32_rt(L, channels, f.M, fma, s);
+        // A batch of channels runs as one launch per channel on the stream: the
+        // channels' persistent sweeps then do not overlap.  One launch with
+        // grid.y = channel measured 3.7 % slower per channel at 8 x 2^28
+        // samples, as the next channel's workgroups start beside the last
+        // ones of the previous (profiles/tuning/r03_batched_ab.txt).
+        for (int c = 0; c < channels && rc == SRCDSP_OK; ++c) {
+            DecimLaunch Lc = L;
+            Lc.in = (const float2 *)L.in + c * L.in_stride;
+            Lc.out = (float2 *)L.out + c * L.out_stride;
+            Lc.hist_in[0] = L.hist_in[c];
+            Lc.hist_out[0] = L.hist_out[c];
+            rc = launch_cf32_compiled(Lc, 1, f.M, f.ntaps, fma, s);
+            if (rc == SRCDSP_ERR_UNSUPPORTED) rc = launch_cf32_rt(Lc, 1, f.M, fma, s);
+        }
     } else if (f.M == 1 && f.kv == KV_F32_REAL && al && out_al && f.ntaps <= kFirMaxTaps && !mixed) {
         rc = launch_fir_tile<KV_F32_REAL>(L, channels, fma, s);
     } else if (f.M == 4 && f.kv == KV_CI16_I32 && f.coef_fits_i16 && al && out_al && (f.ntaps == 127 || f.ntaps == 128)) {

@@ -418,8 +418,9 @@ def test_fir_float_tile_kernel_vs_oracle(S, O, fp, ntaps):
                                        (1, 127, 98304), (3, 128, 98304), (8, 255, 98304), (16, 255, 98304),
                                        (4, 255, 98304), (4, 127, 4 * 24575), (2, 64, 2 * 24575)])
 def test_decim_batched_equals_single(S, O, M, ntaps, L):
-    """The batched launch (grid.y = channel, configs[2]'s layout) on the headline
-    kernel at each compiled (M, taps) and on the any-tap tile kernel: per-channel
+    """The batched step (configs[2]'s layout: one launch per channel on the
+    headline kernel, grid.y = channel elsewhere) at each compiled (M, taps)
+    and on the any-tap tile kernel: per-channel
     history across steps.  An odd output row count makes the output row stride
     8-B aligned only: those launches must leave the 16-B-store kernels."""
     import torch
