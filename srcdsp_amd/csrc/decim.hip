@@ -220,19 +220,24 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
         // BASELINE lengths (127/128: configs 2 and 3) and the common neighbouring
         // power-of-two lengths; any other N <= 1024 takes the same kernel with
         // the tap count at run time
-        // A batch of channels runs as one launch per channel on the stream: the
-        // channels' persistent sweeps then do not overlap.  One launch with
-        // grid.y = channel measured 3.7 % slower per channel at 8 x 2^28
-        // samples, as the next channel's workgroups start beside the last
-        // ones of the previous (profiles/tuning/r03_batched_ab.txt).
-        for (int c = 0; c < channels && rc == SRCDSP_OK; ++c) {
+        // A batch of long channels runs as one launch per channel on the
+        // stream, so the channels' persistent sweeps do not overlap: one launch
+        // with grid.y = channel measured 3.7 % slower per channel at 8 x 2^28
+        // samples, as the next channel's workgroups start beside the last ones
+        // of the previous (profiles/tuning/r03_batched_ab.txt).  Short channels
+        // (under 2^22 samples, where one channel does not fill the persistent
+        // grid for long) keep the single grid.y launch.
+        const int per = (channels > 1 && L.n_in >= (1L << 22)) ? 1 : channels;
+        for (int c = 0; c < channels && rc == SRCDSP_OK; c += per) {
             DecimLaunch Lc = L;
             Lc.in = (const float2 *)L.in + c * L.in_stride;
             Lc.out = (float2 *)L.out + c * L.out_stride;
-            Lc.hist_in[0] = L.hist_in[c];
-            Lc.hist_out[0] = L.hist_out[c];
-            rc = launch_cf32_compiled(Lc, 1, f.M, f.ntaps, fma, s);
-            if (rc == SRCDSP_ERR_UNSUPPORTED) rc = launch_cf32_rt(Lc, 1, f.M, fma, s);
+            for (int k = 0; k < per; ++k) {
+                Lc.hist_in[k] = L.hist_in[c + k];
+                Lc.hist_out[k] = L.hist_out[c + k];
+            }
+            rc = launch_cf32_compiled(Lc, per, f.M, f.ntaps, fma, s);
+            if (rc == SRCDSP_ERR_UNSUPPORTED) rc = launch_cf32_rt(Lc, per, f.M, fma, s);
         }
     } else if (f.M == 1 && f.kv == KV_F32_REAL && al && out_al && f.ntaps <= kFirMaxTaps && !mixed) {
         rc = launch_fir_tile<KV_F32_REAL>(L, channels, fma, s);
