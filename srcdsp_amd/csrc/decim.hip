@@ -99,6 +99,12 @@ int launch_ci16_dot2_shape(DecimLaunch L, int channels, bool mixed, hipStream_t 
     constexpr int TO = BLOCK * kCiR;
     L.ntiles = (L.n_out + TO - 1) / TO;
     if (mixed) L.mix_dtile = phase_step_tile(L.mix_N, L.mix_freq, TO);
+    if (mixed && NT == 0) {
+        // phase of tile 0's first staged sample, -dot2_rt_halo(N) (the
+        // caller's value is for the 127/128-tap halo of 128 samples)
+        const unsigned long N = L.mix_N, h = (unsigned long)dot2_rt_halo(L.ntaps) % N;
+        L.mix_phase_tile0 = (unsigned)((L.mix_phase0 + ((N - h) % N) * L.mix_freq) % N);
+    }
     if (mixed && TABM == 2) {
         L.mix_pe = mixer_seq_period(L.mix_N, L.mix_freq);
         L.mix_pe_dtile = (unsigned)((4ul * TO) % L.mix_pe);
@@ -241,20 +247,23 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
         }
     } else if (f.M == 1 && f.kv == KV_F32_REAL && al && out_al && f.ntaps <= kFirMaxTaps && !mixed) {
         rc = launch_fir_tile<KV_F32_REAL>(L, channels, fma, s);
-    } else if (f.M == 4 && f.kv == KV_CI16_I32 && f.coef_fits_i16 && al && out_al && (f.ntaps == 127 || f.ntaps == 128)) {
+    } else if (f.M == 4 && f.kv == KV_CI16_I32 && f.coef_fits_i16 && al && out_al && f.ntaps <= kDot2MaxTaps) {
+        // complex<int16_t> x int16-range taps on v_dot2 tap pairs, the mixer
+        // fused when chained: the tap count compiled in at 127/128 (configs 4)
+        // and, unmixed, 63/64/255/256; any other N <= kDot2MaxTaps at run time
         DecimLaunch L2 = L;
         L2.coef = f.d_cpair;
-        rc = f.ntaps == 127 ? launch_ci16_dot2<127>(L2, channels, mixed, s) : launch_ci16_dot2<128>(L2, channels, mixed, s);
-    } else if (f.M == 4 && f.kv == KV_CI16_I32 && f.coef_fits_i16 && al && out_al && !mixed &&
-               (f.ntaps == 63 || f.ntaps == 64 || f.ntaps == 255 || f.ntaps == 256)) {
-        // the dot2 kernel's product shape at the neighbouring power-of-two lengths
-        DecimLaunch L2 = L;
-        L2.coef = f.d_cpair;
-        switch (f.ntaps) {
-        case 63: rc = launch_ci16_dot2_shape<63, 512, 0>(L2, channels, false, s); break;
-        case 64: rc = launch_ci16_dot2_shape<64, 512, 0>(L2, channels, false, s); break;
-        case 255: rc = launch_ci16_dot2_shape<255, 512, 0>(L2, channels, false, s); break;
-        default: rc = launch_ci16_dot2_shape<256, 512, 0>(L2, channels, false, s); break;
+        if (f.ntaps == 127 || f.ntaps == 128) {
+            rc = f.ntaps == 127 ? launch_ci16_dot2<127>(L2, channels, mixed, s) : launch_ci16_dot2<128>(L2, channels, mixed, s);
+        } else if (!mixed && (f.ntaps == 63 || f.ntaps == 64 || f.ntaps == 255 || f.ntaps == 256)) {
+            switch (f.ntaps) {
+            case 63: rc = launch_ci16_dot2_shape<63, 512, 0>(L2, channels, false, s); break;
+            case 64: rc = launch_ci16_dot2_shape<64, 512, 0>(L2, channels, false, s); break;
+            case 255: rc = launch_ci16_dot2_shape<255, 512, 0>(L2, channels, false, s); break;
+            default: rc = launch_ci16_dot2_shape<256, 512, 0>(L2, channels, false, s); break;
+            }
+        } else {
+            rc = launch_ci16_dot2<0>(L2, channels, mixed, s);
         }
     } else if (f.M == 4 && f.kv == KV_CI16_I32 && f.coef_fits_i24 && al && out_al && (f.ntaps == 127 || f.ntaps == 128)) {
         rc = f.ntaps == 127 ? launch_ci16<127>(L, channels, mixed, s) : launch_ci16<128>(L, channels, mixed, s);
@@ -274,7 +283,8 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
             rc = launch_decim_tile_m<KV_CI16_I32, 1>(L, channels, f.M, s);
     } else {
         if (mixed) {
-            set_error("mixer->decimator fusion needs variant 1, M=4, 127/128 taps |c|<2^23, 16-B aligned input and output");
+            set_error("mixer->decimator fusion needs variant 1, M=4, int16-range taps (N <= 1024) or 127/128 taps |c|<2^23, "
+                      "16-B aligned input and output");
             return SRCDSP_ERR_UNSUPPORTED;
         }
         switch (f.kv) {
@@ -331,11 +341,13 @@ int FirCore::set_coeffs(const void *coeffs, int n, bool keep_history) {
     if (coef_fits_i16) {  // tap pairs for v_dot2: P_j = (lo c[2j], hi c[2j-1]), c[-1] = c[n] = 0
         const int32_t *c = (const int32_t *)tmp.data();
         auto tap = [&](int k) { return (k >= 0 && k < n) ? (uint32_t)(uint16_t)(int16_t)c[k] : 0u; };
-        const int J = n / 2 + 1;
-        std::vector<uint32_t> pr((size_t)J);
+        // zero pairs after the N/2+1 real ones: the run-time-tap kernel's
+        // padded steps and its chunks' 16-pair s_loads read them
+        const int J = n / 2 + 1, JA = std::max(J, dot2_pair_alloc(n));
+        std::vector<uint32_t> pr((size_t)JA, 0u);
         for (int j = 0; j < J; ++j) pr[j] = tap(2 * j) | (tap(2 * j - 1) << 16);
-        SRCDSP_HIP_TRY(hipMalloc(&d_cpair, 4 * (size_t)J));
-        SRCDSP_HIP_TRY(hipMemcpy(d_cpair, pr.data(), 4 * (size_t)J, hipMemcpyHostToDevice));
+        SRCDSP_HIP_TRY(hipMalloc(&d_cpair, 4 * (size_t)JA));
+        SRCDSP_HIP_TRY(hipMemcpy(d_cpair, pr.data(), 4 * (size_t)JA, hipMemcpyHostToDevice));
     }
     // 32 zero taps of slack: the tap chunks of decim_tile end on 12/16/20-tap
     // boundaries (taps past N are never applied, but their s_load stays in bounds)
@@ -737,8 +749,9 @@ SRCDSP_API int srcdsp_mixdecim_step(srcdsp_mixer_t mixer, srcdsp_decim_t decim, 
     if (n_in == 0) return SRCDSP_OK;
     SRCDSP_ARG_CHECK(d_in && d_out, "mixdecim_step: null buffer");
     hipStream_t s = (hipStream_t)stream;
-    // fused: variant 1, M = 4, 127/128 taps with |c| < 2^23, a table of <= 4096
-    // entries, 16-B aligned buffers (decim_launch refuses the rest unchanged)
+    // fused: variant 1, M = 4, int16-range taps (any N <= 1024) or 127/128 taps
+    // with |c| < 2^23, a table of <= 4096 entries, 16-B aligned buffers
+    // (decim_launch refuses the rest unchanged)
     if (f.kv != KV_CI16_I32 || m.N > 4096) return mixdecim_unfused(mixer, f, d_in, n_in, d_out, n_out, s);
     int rc = m.order.before(s);
     if (rc) return rc;

@@ -1098,6 +1098,18 @@ __device__ __forceinline__ int dot2_slot(int G, int pl) {
     static_assert(NC % 8 == 4, "2 NC = 8 (mod 16): conflict-free staging writes");
     return pl * 2 * NC + (G & 1) * NC + (G >> 1);
 }
+// run-time tap count (decim_dot2_ci16<0, ...>): N <= kDot2MaxTaps; tap pairs
+// padded with zero pairs to whole 4-pair steps (exact: integer products of a
+// zero pair add 0), and the halo of that padded count plus one plane granule
+// pair (the window granule read one step ahead of the last step)
+constexpr int kDot2MaxTaps = 1024;
+__host__ __device__ constexpr int dot2_rt_pairs(int ntaps) { return 4 * ceildiv(ntaps / 2 + 1, 4); }
+__host__ __device__ constexpr int dot2_rt_halo(int ntaps) {
+    return 16 * ceildiv(2 * (dot2_rt_pairs(ntaps) - 1), 16) + 16;
+}
+// device tap-pair array length: the s_load of a chunk's 16 pairs may reach 12
+// pairs past the padded count
+__host__ __device__ constexpr int dot2_pair_alloc(int ntaps) { return dot2_rt_pairs(ntaps) + 16; }
 __device__ __forceinline__ int32_t clamp_s14(int32_t v) {
     const int32_t a = v >> 14;  // |v| < 2^30: never INT_MIN
     return a > 32767 ? 32767 : (a < -32767 ? -32767 : a);
@@ -1345,20 +1357,29 @@ __global__ __launch_bounds__(kDtBlock) void decim_tile(DecimLaunch a) {
 template <int NT, int BLOCK, bool MIX, int MINW, int TABM = 0>
 __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     constexpr bool TAB2 = TABM == 1, SEQT = TABM == 2;
+    constexpr bool RT = NT == 0;                  // the tap count at run time (a.ntaps <= kDot2MaxTaps)
     constexpr int R = 4;
-    constexpr int J = NT / 2 + 1;                 // tap pairs
-    constexpr int HS = 16 * ceildiv(2 * (J - 1), 16);  // halo samples (lane-chunk aligned)
-    constexpr int HG = HS / 8;                    // halo plane granules
     constexpr int TO = BLOCK * R;                 // outputs per tile
-    constexpr int TG = (4 * TO + HS) / 4;         // staged 16-B sample granules
-    constexpr int PER = ceildiv(TG, BLOCK);
-    constexpr int PG = (4 * TO + HS) / 8;         // plane granules
+    // compile-time geometry: the tap count's, or (RT) the largest tap count's,
+    // which sizes the prefetch registers and the LDS image (its row length NC
+    // then fixed, so every window read is a per-lane base plus immediates)
+    constexpr int JC = RT ? dot2_rt_pairs(kDot2MaxTaps) : NT / 2 + 1;
+    constexpr int HSC = RT ? dot2_rt_halo(kDot2MaxTaps) : 16 * ceildiv(2 * (JC - 1), 16);
+    constexpr int PER = ceildiv((4 * TO + HSC) / 4, BLOCK);
+    constexpr int PG = (4 * TO + HSC) / 8;        // plane granules
     constexpr int NC0 = ceildiv(PG, 2);
     constexpr int NC = NC0 + ((4 - NC0 % 8) + 8) % 8;  // slots per plane row, = 4 (mod 8)
     constexpr int LSLOTS = 4 * NC;
     constexpr int TABMAX = MIX ? (TABM ? 8192 : 4096) : 1;
-    static_assert(HS % 16 == 0 && 2 * (J - 1) <= HS, "halo geometry");
-    static_assert(HG % 2 == 0 && BLOCK % 16 == 0, "column-major plane layout");
+    static_assert(HSC % 16 == 0 && 2 * (JC - 1) <= HSC, "halo geometry");
+    static_assert(BLOCK % 16 == 0, "column-major plane layout");
+    // tap pairs (RT: padded with zero pairs to whole 4-pair steps), halo
+    // samples (lane-chunk aligned; RT: one more plane granule pair, so the
+    // window read one step ahead stays inside the image), staged granules
+    const int J = RT ? dot2_rt_pairs(a.ntaps) : JC;
+    const int HS = RT ? dot2_rt_halo(a.ntaps) : HSC;
+    const int HG = HS / 8;                        // halo plane granules (even)
+    const int TG = (4 * TO + HS) / 4;             // staged 16-B sample granules
     __shared__ uint4 lds[LSLOTS];
     __shared__ __attribute__((aligned(16))) uint32_t ctab[TABMAX];
 
@@ -1367,7 +1388,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     const uint32_t *hist = (const uint32_t *)a.hist_in[ch];
     uint32_t *out = (uint32_t *)a.out + ch * a.out_stride;
     const long n_in = a.n_in;
-    const int H = NT - 1;
+    const int H = RT ? a.ntaps - 1 : NT - 1;
     const int t = threadIdx.x;
     const unsigned N = a.mix_N, fr = a.mix_freq;
     const long nb = gridDim.x;
@@ -1525,7 +1546,6 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
             stage_load(t_begin);
         }
     }
-    const int lb = 2 * t + HG;  // lane's first plane granule
     for (long tile = t_begin; tile < t_end; ++tile) {
         SRCDSP_LDS_BARRIER();
         if (MIX && SEQT && tile != 0) {
@@ -1565,37 +1585,108 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
 
         ConstPtr<uint32_t> tp = const_view<uint32_t>(a.coef);
         asm volatile("" : "+s"(tp));
-        // window: Dr[d + OFF], d in [-(4*NG), 8), NG = granules below the lane base
-        constexpr int NG = ceildiv(J - 1, 4);
-        constexpr int OFF = 4 * NG;
-        uint32_t Dr[OFF + 8], Di[OFF + 8];
-        auto load_g = [&](int c) {  // plane granule lb + c -> dwords d = 4c .. 4c+3
-            typedef uint32_t u4v_t __attribute__((ext_vector_type(4)));
-            // granule lb + c = 2t + HG + c: row c & 1, column t + (HG + c) >> 1
-            const int o = (c & 1) * NC + ((HG + c) >> 1);
-            u4v_t gr = *(const u4v_t *)&lds[t + o];
-            u4v_t gi = *(const u4v_t *)&lds[t + o + 2 * NC];
-            // keep every read a whole ds_read_b128: at the window edges the
-            // compiler would load only the words used, as ds_read2_b32 /
-            // ds_read_b96, whose 4-B lane groups the layout does not spread
-            asm volatile("" : "+v"(gr), "+v"(gi));
-            Dr[OFF + 4 * c + 0] = gr[0]; Dr[OFF + 4 * c + 1] = gr[1]; Dr[OFF + 4 * c + 2] = gr[2]; Dr[OFF + 4 * c + 3] = gr[3];
-            Di[OFF + 4 * c + 0] = gi[0]; Di[OFF + 4 * c + 1] = gi[1]; Di[OFF + 4 * c + 2] = gi[2]; Di[OFF + 4 * c + 3] = gi[3];
-        };
-        load_g(0);
-        load_g(1);
+        typedef uint32_t u4v_t __attribute__((ext_vector_type(4)));
         int32_t yr[R], yi[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) yr[r] = yi[r] = 0;
+        if constexpr (!RT) {
+            // window: Dr[d + OFF], d in [-(4*NG), 8), NG = granules below the lane base
+            constexpr int NG = ceildiv(JC - 1, 4);
+            constexpr int OFF = 4 * NG;
+            uint32_t Dr[OFF + 8], Di[OFF + 8];
+            auto load_g = [&](int c) {  // plane granule lb + c -> dwords d = 4c .. 4c+3
+                // granule lb + c = 2t + HG + c: row c & 1, column t + (HG + c) >> 1
+                const int o = (c & 1) * NC + ((HG + c) >> 1);
+                u4v_t gr = *(const u4v_t *)&lds[t + o];
+                u4v_t gi = *(const u4v_t *)&lds[t + o + 2 * NC];
+                // keep every read a whole ds_read_b128: at the window edges the
+                // compiler would load only the words used, as ds_read2_b32 /
+                // ds_read_b96, whose 4-B lane groups the layout does not spread
+                asm volatile("" : "+v"(gr), "+v"(gi));
+                Dr[OFF + 4 * c + 0] = gr[0]; Dr[OFF + 4 * c + 1] = gr[1]; Dr[OFF + 4 * c + 2] = gr[2]; Dr[OFF + 4 * c + 3] = gr[3];
+                Di[OFF + 4 * c + 0] = gi[0]; Di[OFF + 4 * c + 1] = gi[1]; Di[OFF + 4 * c + 2] = gi[2]; Di[OFF + 4 * c + 3] = gi[3];
+            };
+            load_g(0);
+            load_g(1);
 #pragma unroll
-        for (int j = 0; j < J; ++j) {
-            if ((j & 3) == 1) load_g(-1 - (j >> 2));
-            if ((j & 15) == 0) asm volatile("" : "+s"(tp));
-            const uint32_t P = tp[j];
+            for (int j = 0; j < JC; ++j) {
+                if ((j & 3) == 1) load_g(-1 - (j >> 2));
+                if ((j & 15) == 0) asm volatile("" : "+s"(tp));
+                const uint32_t P = tp[j];
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                yr[r] = sdot2(Dr[OFF + 2 * r - j], P, yr[r]);
-                yi[r] = sdot2(Di[OFF + 2 * r - j], P, yi[r]);
+                for (int r = 0; r < R; ++r) {
+                    yr[r] = sdot2(Dr[OFF + 2 * r - j], P, yr[r]);
+                    yi[r] = sdot2(Di[OFF + 2 * r - j], P, yi[r]);
+                }
+            }
+        } else {
+            // Run-time tap count: steps of 4 pairs; step q (pairs 4q..4q+3)
+            // reads window granules -q-1, -q, -q+1 (dword 2r - j of granule
+            // floor((2r - j) / 4)) and loads -q-2 for the next step, so 4
+            // register slots (granule c in slot c mod 4) rotate with static
+            // names over chunks of 4 steps (16 pairs: one s_load_dwordx16).
+            // A chunk starting at step q0 (a multiple of 4, so granule parity
+            // is static) reads granule e - q0 at column t + (HG - q0)/2 +
+            // floor(e/2) of row e & 1: one base per chunk plus immediates.
+            uint32_t W[4][2][4];  // [slot][plane][dword]
+            auto slot = [](int e) { return ((e % 4) + 4) % 4; };
+            auto load_e = [&](int cb, int e) {
+                const int o = cb + (e & 1) * NC + (e >> 1);
+                u4v_t gr = *(const u4v_t *)&lds[o];
+                u4v_t gi = *(const u4v_t *)&lds[o + 2 * NC];
+                asm volatile("" : "+v"(gr), "+v"(gi));  // whole ds_read_b128 (as above)
+                uint32_t(&w)[2][4] = W[slot(e)];
+                w[0][0] = gr[0]; w[0][1] = gr[1]; w[0][2] = gr[2]; w[0][3] = gr[3];
+                w[1][0] = gi[0]; w[1][1] = gi[1]; w[1][2] = gi[2]; w[1][3] = gi[3];
+            };
+            const int NS = J / 4;  // steps
+            // a chunk's 16 tap pairs are requested one chunk ahead (the pair
+            // array has 16 zero pairs of slack past the padded count), so the
+            // lgkmcnt wait for a window read never waits on a fresh s_load
+            uint32_t Tc[16], Tn[16];
+            auto load_taps = [&](uint32_t(&T)[16], int q0) {
+                ConstPtr<uint32_t> tc = tp + 4 * q0;
+                asm volatile("" : "+s"(tc));
+#pragma unroll
+                for (int i = 0; i < 16; ++i) T[i] = tc[i];
+            };
+            load_taps(Tc, 0);
+            auto chunk = [&](int q0, auto steps_tag) {
+                constexpr int SN = decltype(steps_tag)::value;  // steps in this chunk (4, or a tail 1..3)
+                const int cb = t + ((HG - q0) >> 1);
+#pragma unroll
+                for (int s = 0; s < SN; ++s) {
+                    load_e(cb, -s - 2);
+                    if (SN == 4 && s == 0) load_taps(Tn, q0 + 4);
+#pragma unroll
+                    for (int p = 0; p < 4; ++p) {
+                        const uint32_t P = Tc[4 * s + p];
+#pragma unroll
+                        for (int r = 0; r < R; ++r) {
+                            const int d = 2 * r - 4 * s - p, e = floordiv(d, 4);
+                            yr[r] = sdot2(W[slot(e)][0][d - 4 * e], P, yr[r]);
+                            yi[r] = sdot2(W[slot(e)][1][d - 4 * e], P, yi[r]);
+                        }
+                    }
+                }
+                if constexpr (SN == 4) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) Tc[i] = Tn[i];
+                }
+            };
+            {
+                const int cb = t + (HG >> 1);
+                load_e(cb, 1);
+                load_e(cb, 0);
+                load_e(cb, -1);
+            }
+            int q0 = 0;
+            for (; q0 + 4 <= NS; q0 += 4) chunk(q0, std::integral_constant<int, 4>{});
+            switch (NS - q0) {  // wave-uniform
+            case 1: chunk(q0, std::integral_constant<int, 1>{}); break;
+            case 2: chunk(q0, std::integral_constant<int, 2>{}); break;
+            case 3: chunk(q0, std::integral_constant<int, 3>{}); break;
+            default: break;
             }
         }
         const long n0 = tile * TO + (long)t * R;
