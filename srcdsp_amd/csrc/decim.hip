@@ -45,9 +45,9 @@ namespace srcdsp {
 namespace {
 constexpr int kCiR_ = 4, kCiBlock_ = 256;
 }
-// phase advance of the fused mixer per ci16 tile of `to` outputs (4*to samples)
-unsigned phase_step_tile(unsigned long N, unsigned long fr, unsigned long to) {
-    return (unsigned)(((4ul * to) % N) * fr % N);
+// phase advance of the fused mixer over `samples` input samples (one tile)
+unsigned phase_step(unsigned long N, unsigned long fr, unsigned long samples) {
+    return (unsigned)((samples % N) * fr % N);
 }
 namespace {
 // cf32 tiles: 4 outputs per lane, 512 lanes -> 8192 input samples per tile,
@@ -94,11 +94,11 @@ static unsigned mixer_seq_period(unsigned N, unsigned fr) {
 }
 constexpr unsigned kSeqMax = 4096;  // 2 x 4096 words of LDS, as the doubled phase table
 
-template <int NT, int BLOCK, int TABM>
+template <int NT, int BLOCK, int TABM, int MD = 4>
 int launch_ci16_dot2_shape(DecimLaunch L, int channels, bool mixed, hipStream_t s) {
-    constexpr int TO = BLOCK * kCiR;
+    constexpr int TO = BLOCK * dot2_r(MD), SPT = MD * TO;  // outputs / input samples per tile
     L.ntiles = (L.n_out + TO - 1) / TO;
-    if (mixed) L.mix_dtile = phase_step_tile(L.mix_N, L.mix_freq, TO);
+    if (mixed) L.mix_dtile = phase_step(L.mix_N, L.mix_freq, SPT);
     if (mixed && NT == 0) {
         // phase of tile 0's first staged sample, -dot2_rt_halo(N) (the
         // caller's value is for the 127/128-tap halo of 128 samples)
@@ -107,18 +107,18 @@ int launch_ci16_dot2_shape(DecimLaunch L, int channels, bool mixed, hipStream_t 
     }
     if (mixed && TABM == 2) {
         L.mix_pe = mixer_seq_period(L.mix_N, L.mix_freq);
-        L.mix_pe_dtile = (unsigned)((4ul * TO) % L.mix_pe);
+        L.mix_pe_dtile = (unsigned)((unsigned long)SPT % L.mix_pe);
         L.mix_pe_drow = (unsigned)((4ul * BLOCK) % L.mix_pe);
     }
     dim3 grid((unsigned)std::min<long>(L.ntiles, kCfGridCap * 256 / BLOCK), channels);
     if (mixed)
-        hipLaunchKernelGGL((decim_dot2_ci16<NT, BLOCK, true, 4, TABM>), grid, dim3(BLOCK), 0, s, L);
+        hipLaunchKernelGGL((decim_dot2_ci16<NT, BLOCK, true, 4, TABM, MD>), grid, dim3(BLOCK), 0, s, L);
     else
-        hipLaunchKernelGGL((decim_dot2_ci16<NT, BLOCK, false, 4>), grid, dim3(BLOCK), 0, s, L);
+        hipLaunchKernelGGL((decim_dot2_ci16<NT, BLOCK, false, 4, 0, MD>), grid, dim3(BLOCK), 0, s, L);
     return SRCDSP_OK;
 }
 
-template <int NT>
+template <int NT, int MD = 4>
 int launch_ci16_dot2(DecimLaunch L, int channels, bool mixed, hipStream_t s) {
 #ifdef SRCDSP_TUNING
     switch (ci16_variant()) {
@@ -134,8 +134,8 @@ int launch_ci16_dot2(DecimLaunch L, int channels, bool mixed, hipStream_t s) {
     // doubled phase table (only these instantiations are compiled outside the
     // tuning build)
     if (mixed && mixer_seq_period(L.mix_N, L.mix_freq) > kSeqMax)
-        return launch_ci16_dot2_shape<NT, 512, 1>(L, channels, mixed, s);
-    return launch_ci16_dot2_shape<NT, 512, 2>(L, channels, mixed, s);
+        return launch_ci16_dot2_shape<NT, 512, 1, MD>(L, channels, mixed, s);
+    return launch_ci16_dot2_shape<NT, 512, 2, MD>(L, channels, mixed, s);
 }
 
 template <int KV>
@@ -247,13 +247,19 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
         }
     } else if (f.M == 1 && f.kv == KV_F32_REAL && al && out_al && f.ntaps <= kFirMaxTaps && !mixed) {
         rc = launch_fir_tile<KV_F32_REAL>(L, channels, fma, s);
-    } else if (f.M == 4 && f.kv == KV_CI16_I32 && f.coef_fits_i16 && al && out_al && f.ntaps <= kDot2MaxTaps) {
+    } else if ((f.M == 2 || f.M == 4 || f.M == 8 || f.M == 16) && f.kv == KV_CI16_I32 && f.coef_fits_i16 && al &&
+               out_al && f.ntaps <= kDot2MaxTaps) {
         // complex<int16_t> x int16-range taps on v_dot2 tap pairs, the mixer
-        // fused when chained: the tap count compiled in at 127/128 (configs 4)
-        // and, unmixed, 63/64/255/256; any other N <= kDot2MaxTaps at run time
+        // fused when chained: at M = 4 the tap count compiled in at 127/128
+        // (config 4) and, unmixed, 63/64/255/256; any other N <= kDot2MaxTaps
+        // and M = 2 / 8 / 16 at run time
         DecimLaunch L2 = L;
         L2.coef = f.d_cpair;
-        if (f.ntaps == 127 || f.ntaps == 128) {
+        if (f.M != 4) {
+            rc = f.M == 2 ? launch_ci16_dot2<0, 2>(L2, channels, mixed, s)
+                          : (f.M == 8 ? launch_ci16_dot2<0, 8>(L2, channels, mixed, s)
+                                      : launch_ci16_dot2<0, 16>(L2, channels, mixed, s));
+        } else if (f.ntaps == 127 || f.ntaps == 128) {
             rc = f.ntaps == 127 ? launch_ci16_dot2<127>(L2, channels, mixed, s) : launch_ci16_dot2<128>(L2, channels, mixed, s);
         } else if (!mixed && (f.ntaps == 63 || f.ntaps == 64 || f.ntaps == 255 || f.ntaps == 256)) {
             switch (f.ntaps) {
@@ -283,7 +289,8 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
             rc = launch_decim_tile_m<KV_CI16_I32, 1>(L, channels, f.M, s);
     } else {
         if (mixed) {
-            set_error("mixer->decimator fusion needs variant 1, M=4, int16-range taps (N <= 1024) or 127/128 taps |c|<2^23, "
+            set_error("mixer->decimator fusion needs variant 1, M = 2/4/8/16 with int16-range taps (N <= 1024) or M = 4 with "
+                      "127/128 taps |c|<2^23, "
                       "16-B aligned input and output");
             return SRCDSP_ERR_UNSUPPORTED;
         }
@@ -458,7 +465,7 @@ static int core_step(FirCore &f, const void *d_in, size_t n_in, void *d_out, siz
         L.mix_phase0 = (unsigned)phi0;
         L.mix_freq = (unsigned)fr;
         L.mix_phase_tile0 = phase(-4 * kNQ);
-        L.mix_dtile = phase_step_tile(N, fr, (unsigned long)kCiBlock_ * kCiR_);  // reset per kernel tile
+        L.mix_dtile = phase_step(N, fr, 4ul * kCiBlock_ * kCiR_);  // reset per kernel tile
         L.mix_phase_hist = phase((long)n_in - (f.ntaps - 1));
     }
     rc = decim_launch(f, L, 1, s, mix != nullptr);

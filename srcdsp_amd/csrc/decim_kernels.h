@@ -1098,6 +1098,9 @@ __device__ __forceinline__ int dot2_slot(int G, int pl) {
     static_assert(NC % 8 == 4, "2 NC = 8 (mod 16): conflict-free staging writes");
     return pl * 2 * NC + (G & 1) * NC + (G >> 1);
 }
+// outputs per lane of decim_dot2_ci16 at decimation M: a lane chunk is 16
+// input samples (2 plane granules) at every M
+__host__ __device__ constexpr int dot2_r(int M) { return 16 / M; }
 // run-time tap count (decim_dot2_ci16<0, ...>): N <= kDot2MaxTaps; tap pairs
 // padded with zero pairs to whole 4-pair steps (exact: integer products of a
 // zero pair add 0), and the halo of that padded count plus one plane granule
@@ -1107,9 +1110,10 @@ __host__ __device__ constexpr int dot2_rt_pairs(int ntaps) { return 4 * ceildiv(
 __host__ __device__ constexpr int dot2_rt_halo(int ntaps) {
     return 16 * ceildiv(2 * (dot2_rt_pairs(ntaps) - 1), 16) + 16;
 }
-// device tap-pair array length: the s_load of a chunk's 16 pairs may reach 12
-// pairs past the padded count
-__host__ __device__ constexpr int dot2_pair_alloc(int ntaps) { return dot2_rt_pairs(ntaps) + 16; }
+// device tap-pair array length: zero pairs of slack past the padded count for
+// the chunk of up to 24 pairs requested one chunk ahead
+constexpr int dot2_pair_slack = 32;
+__host__ __device__ constexpr int dot2_pair_alloc(int ntaps) { return dot2_rt_pairs(ntaps) + dot2_pair_slack; }
 __device__ __forceinline__ int32_t clamp_s14(int32_t v) {
     const int32_t a = v >> 14;  // |v| < 2^30: never INT_MIN
     return a > 32767 ? 32767 : (a < -32767 ? -32767 : a);
@@ -1354,19 +1358,22 @@ __global__ __launch_bounds__(kDtBlock) void decim_tile(DecimLaunch a) {
 //    Pe only), stored twice (2 Pe words).  A lane's 4 samples are 4
 //    consecutive words: one conflict-free ds_read_b128 per granule, any freq.
 // Products via VOP3 dot2 and the pair clamp above.
-template <int NT, int BLOCK, bool MIX, int MINW, int TABM = 0>
+template <int NT, int BLOCK, bool MIX, int MINW, int TABM = 0, int MD = 4>
 __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     constexpr bool TAB2 = TABM == 1, SEQT = TABM == 2;
     constexpr bool RT = NT == 0;                  // the tap count at run time (a.ntaps <= kDot2MaxTaps)
-    constexpr int R = 4;
+    static_assert(MD == 2 || MD == 4 || MD == 8 || MD == 16, "even M whose lane chunk is whole plane granules");
+    static_assert(MD == 4 || RT, "tap counts are compiled in at M = 4 only");
+    constexpr int R = dot2_r(MD);                 // outputs per lane (a lane chunk: 16 samples)
     constexpr int TO = BLOCK * R;                 // outputs per tile
+    constexpr int SPT = MD * TO;                  // input samples per tile
     // compile-time geometry: the tap count's, or (RT) the largest tap count's,
     // which sizes the prefetch registers and the LDS image (its row length NC
     // then fixed, so every window read is a per-lane base plus immediates)
     constexpr int JC = RT ? dot2_rt_pairs(kDot2MaxTaps) : NT / 2 + 1;
     constexpr int HSC = RT ? dot2_rt_halo(kDot2MaxTaps) : 16 * ceildiv(2 * (JC - 1), 16);
-    constexpr int PER = ceildiv((4 * TO + HSC) / 4, BLOCK);
-    constexpr int PG = (4 * TO + HSC) / 8;        // plane granules
+    constexpr int PER = ceildiv((SPT + HSC) / 4, BLOCK);
+    constexpr int PG = (SPT + HSC) / 8;           // plane granules
     constexpr int NC0 = ceildiv(PG, 2);
     constexpr int NC = NC0 + ((4 - NC0 % 8) + 8) % 8;  // slots per plane row, = 4 (mod 8)
     constexpr int LSLOTS = 4 * NC;
@@ -1379,7 +1386,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     const int J = RT ? dot2_rt_pairs(a.ntaps) : JC;
     const int HS = RT ? dot2_rt_halo(a.ntaps) : HSC;
     const int HG = HS / 8;                        // halo plane granules (even)
-    const int TG = (4 * TO + HS) / 4;             // staged 16-B sample granules
+    const int TG = (SPT + HS) / 4;                // staged 16-B sample granules
     __shared__ uint4 lds[LSLOTS];
     __shared__ __attribute__((aligned(16))) uint32_t ctab[TABMAX];
 
@@ -1439,13 +1446,13 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     }
     const unsigned d_lane = MIX ? phase_add(0, 4 * t) : 0;
     const unsigned d_i = MIX ? phase_add(0, 4 * BLOCK) : 0;
-    auto tile_phase = [&](long tile) {  // phase of the tile's first staged sample 4*tile*TO - HS
+    auto tile_phase = [&](long tile) {  // phase of the tile's first staged sample tile*SPT - HS
         return (a.mix_phase_tile0 + ((unsigned)(tile % N)) * a.mix_dtile) % N;
     };
 
     uint4 v[PER];
     auto stage_load = [&](long tile) {  // tile >= 1
-        const long b0 = 4 * tile * TO - HS;
+        const long b0 = (long)SPT * tile - HS;
         const long remb = (n_in - b0) * 4;
         const unsigned nrec = (unsigned)(remb > 0xfffffff0L ? 0xfffffff0L : (remb < 0 ? 0 : remb));
         __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)(in + b0), 0, nrec, 0x00020000);
@@ -1510,7 +1517,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     // SEQT: (4*tile*TO - HS) mod Pe of the workgroup's current tile
     unsigned m_tile = 0;
     if constexpr (MIX && SEQT)
-        if (t_begin < t_end) m_tile = (unsigned)((4 * t_begin * (long)TO - HS + 4 * (long)Pe * (1 + HS / 4)) % (long)Pe);
+        if (t_begin < t_end) m_tile = (unsigned)((t_begin * (long)SPT - HS + 4 * (long)Pe * (1 + HS / 4)) % (long)Pe);
     auto put_mixed = [&](int g, uint4 w, unsigned ph) {
         if constexpr (MIX) {
             int32_t r0, i0, r1, i1, r2, i2, r3, i3;
@@ -1620,16 +1627,23 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
                 }
             }
         } else {
-            // Run-time tap count: steps of 4 pairs; step q (pairs 4q..4q+3)
-            // reads window granules -q-1, -q, -q+1 (dword 2r - j of granule
-            // floor((2r - j) / 4)) and loads -q-2 for the next step, so 4
-            // register slots (granule c in slot c mod 4) rotate with static
-            // names over chunks of 4 steps (16 pairs: one s_load_dwordx16).
-            // A chunk starting at step q0 (a multiple of 4, so granule parity
-            // is static) reads granule e - q0 at column t + (HG - q0)/2 +
-            // floor(e/2) of row e & 1: one base per chunk plus immediates.
-            uint32_t W[4][2][4];  // [slot][plane][dword]
-            auto slot = [](int e) { return ((e % 4) + 4) % 4; };
+            // Run-time tap count: steps of 4 pairs.  Output r of a lane sits at
+            // dword r M/2 of the lane's plane chunk; pair j reads dword
+            // r M/2 - j, so step q (pairs 4q..4q+3) reads window granules
+            // -q-1 .. -q + EH/4 (EH = (R-1) M/2) and loads -q-2 for the next
+            // step: S = EH/4 + 3 register slots (granule c in slot c mod S)
+            // rotate with static names over chunks of U steps (an even
+            // multiple of S, so granule parity is static; 4U tap pairs,
+            // requested one chunk ahead).  A chunk starting at step q0 reads
+            // granule e - q0 at column t + (HG - q0)/2 + floor(e/2) of row
+            // e & 1: one base per chunk plus immediates.
+            constexpr int EH = (R - 1) * MD / 2;
+            constexpr int S = EH / 4 + 3;
+            constexpr int U = S % 2 ? 2 * S : S;
+            constexpr int TPC = 4 * U;  // tap pairs per chunk
+            static_assert(TPC <= dot2_pair_slack, "the pair array's zero slack covers a chunk read ahead");
+            uint32_t W[S][2][4];  // [slot][plane][dword]
+            auto slot = [](int e) { return ((e % S) + S) % S; };
             auto load_e = [&](int cb, int e) {
                 const int o = cb + (e & 1) * NC + (e >> 1);
                 u4v_t gr = *(const u4v_t *)&lds[o];
@@ -1639,70 +1653,80 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
                 w[0][0] = gr[0]; w[0][1] = gr[1]; w[0][2] = gr[2]; w[0][3] = gr[3];
                 w[1][0] = gi[0]; w[1][1] = gi[1]; w[1][2] = gi[2]; w[1][3] = gi[3];
             };
+            auto chunk_base = [&](int q0) { return t + ((HG - q0) >> 1); };
             const int NS = J / 4;  // steps
-            // a chunk's 16 tap pairs are requested one chunk ahead (the pair
-            // array has 16 zero pairs of slack past the padded count), so the
-            // lgkmcnt wait for a window read never waits on a fresh s_load
-            uint32_t Tc[16], Tn[16];
-            auto load_taps = [&](uint32_t(&T)[16], int q0) {
+            // the lgkmcnt wait for a window read then never waits on a fresh s_load
+            uint32_t Tc[TPC], Tn[TPC];
+            auto load_taps = [&](uint32_t(&T)[TPC], int q0) {
                 ConstPtr<uint32_t> tc = tp + 4 * q0;
                 asm volatile("" : "+s"(tc));
 #pragma unroll
-                for (int i = 0; i < 16; ++i) T[i] = tc[i];
+                for (int i = 0; i < TPC; ++i) T[i] = tc[i];
             };
             load_taps(Tc, 0);
             auto chunk = [&](int q0, auto steps_tag) {
-                constexpr int SN = decltype(steps_tag)::value;  // steps in this chunk (4, or a tail 1..3)
-                const int cb = t + ((HG - q0) >> 1);
+                constexpr int SN = decltype(steps_tag)::value;  // steps in this chunk (U, or a tail 1..U-1)
+                const int cb = chunk_base(q0);
 #pragma unroll
                 for (int s = 0; s < SN; ++s) {
                     load_e(cb, -s - 2);
-                    if (SN == 4 && s == 0) load_taps(Tn, q0 + 4);
+                    if (SN == U && s == 0) load_taps(Tn, q0 + U);
 #pragma unroll
                     for (int p = 0; p < 4; ++p) {
                         const uint32_t P = Tc[4 * s + p];
 #pragma unroll
                         for (int r = 0; r < R; ++r) {
-                            const int d = 2 * r - 4 * s - p, e = floordiv(d, 4);
+                            const int d = r * MD / 2 - 4 * s - p, e = floordiv(d, 4);
                             yr[r] = sdot2(W[slot(e)][0][d - 4 * e], P, yr[r]);
                             yi[r] = sdot2(W[slot(e)][1][d - 4 * e], P, yi[r]);
                         }
                     }
                 }
-                if constexpr (SN == 4) {
+                if constexpr (SN == U) {
 #pragma unroll
-                    for (int i = 0; i < 16; ++i) Tc[i] = Tn[i];
+                    for (int i = 0; i < TPC; ++i) Tc[i] = Tn[i];
                 }
             };
             {
-                const int cb = t + (HG >> 1);
-                load_e(cb, 1);
-                load_e(cb, 0);
-                load_e(cb, -1);
+                const int cb = chunk_base(0);
+#pragma unroll
+                for (int e = EH / 4; e >= -1; --e) load_e(cb, e);
             }
             int q0 = 0;
-            for (; q0 + 4 <= NS; q0 += 4) chunk(q0, std::integral_constant<int, 4>{});
-            switch (NS - q0) {  // wave-uniform
-            case 1: chunk(q0, std::integral_constant<int, 1>{}); break;
-            case 2: chunk(q0, std::integral_constant<int, 2>{}); break;
-            case 3: chunk(q0, std::integral_constant<int, 3>{}); break;
-            default: break;
-            }
+            for (; q0 + U <= NS; q0 += U) chunk(q0, std::integral_constant<int, U>{});
+            // the tail: 1 .. U-1 steps (wave-uniform), one unrolled body per length
+            auto tail = [&](auto self, auto k_tag) {
+                constexpr int K = decltype(k_tag)::value;
+                if constexpr (K < U) {
+                    if (NS - q0 == K) chunk(q0, k_tag);
+                    else self(self, std::integral_constant<int, K + 1>{});
+                }
+            };
+            tail(tail, std::integral_constant<int, 1>{});
         }
         const long n0 = tile * TO + (long)t * R;
         const unsigned sh = a.shift;
-        if (n0 + R <= a.n_out && (sh & 31u) != 0) {  // Q14 taps: shift 14 (the common case)
-            *(uint4 *)(out + n0) = make_uint4(limit16_pair_sh(yr[0], yi[0], sh), limit16_pair_sh(yr[1], yi[1], sh),
-                                              limit16_pair_sh(yr[2], yi[2], sh), limit16_pair_sh(yr[3], yi[3], sh));
-        } else if (n0 + R <= a.n_out) {
-            *(uint4 *)(out + n0) = make_uint4(pack16(limit16(yr[0], sh), limit16(yi[0], sh)),
-                                              pack16(limit16(yr[1], sh), limit16(yi[1], sh)),
-                                              pack16(limit16(yr[2], sh), limit16(yi[2], sh)),
-                                              pack16(limit16(yr[3], sh), limit16(yi[3], sh)));
+        uint32_t w[R];
+        if ((sh & 31u) != 0) {  // Q14 taps: shift 14 (the common case)
+#pragma unroll
+            for (int r = 0; r < R; ++r) w[r] = limit16_pair_sh(yr[r], yi[r], sh);
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r) w[r] = pack16(limit16(yr[r], sh), limit16(yi[r], sh));
+        }
+        if (n0 + R <= a.n_out) {
+            if constexpr (R >= 4) {
+#pragma unroll
+                for (int r = 0; r < R; r += 4) *(uint4 *)(out + n0 + r) = make_uint4(w[r], w[r + 1], w[r + 2], w[r + 3]);
+            } else if constexpr (R == 2) {
+                *(uint2 *)(out + n0) = make_uint2(w[0], w[1]);
+            } else {
+                out[n0] = w[0];
+            }
         } else {
 #pragma unroll
             for (int r = 0; r < R; ++r)
-                if (n0 + r < a.n_out) out[n0 + r] = pack16(limit16(yr[r], sh), limit16(yi[r], sh));
+                if (n0 + r < a.n_out) out[n0 + r] = w[r];
         }
     }
 }

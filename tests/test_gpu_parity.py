@@ -211,44 +211,55 @@ def test_decim_ci16_dot2_tap_counts_vs_oracle(S, O, ntaps):
 DOT2_RT_TAPS = [1, 2, 3, 5, 17, 31, 62, 65, 100, 126, 129, 200, 257, 300, 511, 600, 1000, 1023, 1024]
 
 
-@pytest.mark.parametrize("ntaps", DOT2_RT_TAPS)
-def test_decim_ci16_dot2_runtime_taps_vs_oracle(S, O, ntaps):
+DOT2_RT_SHAPES = ([(4, n) for n in DOT2_RT_TAPS] +
+                  [(2, n) for n in (1, 2, 7, 31, 63, 64, 65, 127, 200, 1024)] +
+                  [(8, n) for n in (1, 9, 63, 127, 128, 255, 300, 1024)] +
+                  [(16, n) for n in (1, 17, 127, 255, 256, 511, 1024)])
+
+
+@pytest.mark.parametrize("M,ntaps", DOT2_RT_SHAPES)
+def test_decim_ci16_dot2_runtime_taps_vs_oracle(S, O, M, ntaps):
     """The v_dot2 decimator with the tap count at run time (int16-range taps,
-    M = 4, any N <= 1024 off the compiled 63/64/127/128/255/256): the pairs
-    padded with zero pairs to whole 4-pair steps, chunk tails of 1-3 steps,
-    the longest halos; full-scale inputs (accumulator wrap, saturation), a
-    call shorter than the filter, history carried over uneven calls."""
-    rng = np.random.default_rng(2000 + ntaps)
+    any N <= 1024 at M = 2, 8, 16, and at M = 4 off the compiled
+    63/64/127/128/255/256): the pairs padded with zero pairs to whole 4-pair
+    steps, chunk tails, the longest halos; full-scale inputs (accumulator
+    wrap, saturation), a call shorter than the filter, history carried over
+    uneven calls."""
+    rng = np.random.default_rng(2000 + 7 * M + ntaps)
     c = rng.integers(-32768, 32768, size=ntaps).astype(np.int32)
     c[0], c[-1] = 32767, -32768 if ntaps > 1 else 32767
-    x = O["strict"].gen_ci16(31 + ntaps, 4, 0, 600000, -32768, 32767)
-    g = S.FilterDnsamplingFir(c, 4, "complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int32_t")
-    r = O["strict"].decim(1, 4, c)
-    for off, n in _chunks(len(x), [200000, 8, 2048 * 4 + 4, 4 * ((ntaps + 3) // 4) // 2 * 2 + 4, 131072, 128]):
-        n -= n % 4
+    x = O["strict"].gen_ci16(31 + ntaps + M, 4, 0, 600000, -32768, 32767)
+    g = S.FilterDnsamplingFir(c, M, "complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int32_t")
+    r = O["strict"].decim(1, M, c)
+    for off, n in _chunks(len(x), [200000, 8 * M, 2048 * M + 4 * M, M * ((ntaps + 3) // 4) + M, 131072, 128]):
+        n -= n % M
         xs = x[off:off + n]
         assert np.array_equal(g.step(dev(xs)).cpu().numpy(), r.step(xs)), (off, n)
 
 
-@pytest.mark.parametrize("ntaps,N,f", [(1, 4096, 0.1), (31, 4096, 0.1), (63, 1000, -0.37), (64, 4096, 0.5),
-                                       (129, 4096, 0.1), (200, 3000, 0.3), (255, 4093, 0.1), (1024, 4096, 0.73)])
-def test_mixdecim_chain_runtime_taps(S, O, ntaps, N, f):
-    """Config 4's fused mixer -> decimator at tap counts off the compiled
-    127/128 (the run-time-tap dot2 kernel with the mixer in its staging pass),
-    both mixer table forms (N = 4093 at f = 0.1: the doubled phase table), Q14
-    taps of the design filter and full-scale inputs; the same outputs and
-    mixer state as the two reference calls."""
+@pytest.mark.parametrize("M,ntaps,N,f", [(4, 1, 4096, 0.1), (4, 31, 4096, 0.1), (4, 63, 1000, -0.37),
+                                         (4, 64, 4096, 0.5), (4, 129, 4096, 0.1), (4, 200, 3000, 0.3),
+                                         (4, 255, 4093, 0.1), (4, 1024, 4096, 0.73), (2, 63, 4096, 0.1),
+                                         (2, 127, 4093, -0.2), (8, 127, 4096, 0.1), (8, 255, 1000, 0.37),
+                                         (16, 255, 4096, 0.1), (16, 1024, 4093, 0.3)])
+def test_mixdecim_chain_runtime_taps(S, O, M, ntaps, N, f):
+    """Config 4's fused mixer -> decimator off the compiled M = 4 x 127/128:
+    the run-time-tap dot2 kernel with the mixer in its staging pass at
+    M = 2, 4, 8, 16, both mixer table forms (N = 4093 at f = 0.1 / -0.2 /
+    0.3: the doubled phase table), Q14 taps of the design filter and
+    full-scale inputs; the same outputs and mixer state as the two
+    reference calls."""
     from srcdsp_amd.design import hamming_sinc, q14
     cq = q14(hamming_sinc(ntaps)) if ntaps > 1 else np.array([16384], np.int32)
     x = O["strict"].gen_ci16(0xF00 + ntaps, 3, 0, 400000, -32768, 32767)
     m = S.Mixer(N)
     m.reset(f)
-    d = S.FilterDnsamplingFir(cq, 4, "complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int32_t")
+    d = S.FilterDnsamplingFir(cq, M, "complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int32_t")
     chain = S.MixerDecimatorChain(m, d)
-    om, od = O["strict"].mixer(N), O["strict"].decim(1, 4, cq)
+    om, od = O["strict"].mixer(N), O["strict"].decim(1, M, cq)
     om.reset(f)
-    for off, n in _chunks(len(x), [131072, 8, 4100, 200000]):
-        n -= n % 4
+    for off, n in _chunks(len(x), [131072, 8 * M, 4100, 200000]):
+        n -= n % M
         xs = x[off:off + n]
         assert np.array_equal(chain.step(dev(xs)).cpu().numpy(), od.step(om.step(xs))), (off, n)
         assert m.state()[:2] == om.state()[:2]
@@ -354,19 +365,19 @@ def test_mixdecim_chain_table_sizes(S, O, N, f):
         assert m.state()[:2] == om.state()[:2]
 
 
-@pytest.mark.parametrize("case", ["m2", "t63_i24", "t16taps", "wide_taps", "n8192", "out_offset", "in_offset"])
+@pytest.mark.parametrize("case", ["m3", "t63_i24", "t16taps", "wide_taps", "n8192", "out_offset", "in_offset"])
 def test_mixdecim_chain_unfused_configs(S, O, case):
     """Chain configurations the fused kernels do not cover run as the two
     reference calls (mixer launch into a stream-ordered scratch buffer, then the
-    decimator): M = 2, 63 taps beyond the int16 range (the fused v_mad_i32_i24
+    decimator): M = 3, 63 taps beyond the int16 range (the fused v_mad_i32_i24
     kernel is compiled for 127/128 only), int16 taps (variant 2), taps beyond
     2^23, a table of 8192 entries, 4-B-offset output / input views.  Same
     outputs and the same mixer and decimator state as the two oracle calls."""
     import torch
     from srcdsp_amd.design import hamming_sinc, q14
     M, ntaps, N, variant = 4, 127, 4096, 1
-    if case == "m2":
-        M = 2
+    if case == "m3":
+        M = 3
     elif case == "t63_i24":
         ntaps = 63
     elif case == "t16taps":
@@ -407,10 +418,10 @@ def test_mixdecim_chain_unfused_configs(S, O, case):
         assert m.state()[:2] == om.state()[:2]
 
 
-@pytest.mark.parametrize("M,ntaps", [(4, 127), (2, 127)])
+@pytest.mark.parametrize("M,ntaps", [(4, 127), (2, 127), (3, 127)])
 def test_mixdecim_chain_alternating_streams(S, O, M, ntaps):
     """Chain steps issued on two streams in turn with no host synchronisation
-    between them: the handles' stream ordering (and, for the unfused M = 2
+    between them: the handles' stream ordering (and, for the unfused M = 3
     chain, the stream-ordered scratch buffer) keep every step in call order.
     Bit-exact against the two oracle calls."""
     import torch
