@@ -18,13 +18,15 @@ import srcdsp_amd as S  # noqa: E402
 from srcdsp_amd.design import hamming_sinc  # noqa: E402
 
 COMPILED = {4: (63, 64, 127, 128), 8: (127, 128, 255, 256), 16: (127, 128, 255, 256),
-            2: (63, 64, 127, 128), 3: (63, 64, 127, 128), 1: (63, 64)}
+            2: (63, 64, 127, 128), 3: (63, 64, 127, 128), 1: (63, 64), 6: (), 12: ()}
 SHAPES = {4: (31, 63, 95, 100, 126, 127, 129, 200, 255, 300, 511, 1024),
           1: (31, 62, 63, 100, 127, 129, 255, 300),
           2: (62, 63, 95, 127, 129, 200),
           3: (62, 63, 100, 127, 129),
           8: (126, 127, 129, 200, 255, 300),
-          16: (126, 127, 129, 255, 300)}
+          16: (126, 127, 129, 255, 300),
+          6: (31, 63, 127, 255),
+          12: (63, 127, 255)}
 
 
 def main():

@@ -12,7 +12,9 @@ int launch_cf32_rt(DecimLaunch L, int channels, unsigned M, bool fma, hipStream_
     case 2: return launch_cf32<0, 2>(L, channels, fma, s);
     case 3: return launch_cf32<0, 3>(L, channels, fma, s);
     case 4: return launch_cf32<0, 4>(L, channels, fma, s);
+    case 6: return launch_cf32<0, 6>(L, channels, fma, s);
     case 8: return launch_cf32<0, 8>(L, channels, fma, s);
+    case 12: return launch_cf32<0, 12>(L, channels, fma, s);
     default: return launch_cf32<0, 16>(L, channels, fma, s);
     }
 }

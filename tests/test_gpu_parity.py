@@ -104,14 +104,15 @@ def test_decim_cf32_any_taps_tile_vs_oracle(S, O, fp, M, ntaps):
 
 RT_SHAPES = [(4, n) for n in (1, 2, 5, 31, 95, 100, 129, 200, 300, 511, 700, 1024)] + \
     [(1, n) for n in (1, 31, 100, 300, 1024)] + [(2, n) for n in (3, 95, 200, 513)] + \
-    [(3, n) for n in (4, 50, 301)] + [(8, n) for n in (7, 129, 1000)] + [(16, n) for n in (9, 200, 1023)]
+    [(3, n) for n in (4, 50, 301)] + [(8, n) for n in (7, 129, 1000)] + [(16, n) for n in (9, 200, 1023)] + \
+    [(6, n) for n in (1, 13, 127, 600)] + [(12, n) for n in (5, 127, 1024)]
 
 
 @pytest.mark.parametrize("fp", ["fma", "strict"])
 @pytest.mark.parametrize("M,ntaps", RT_SHAPES)
 def test_decim_cf32_runtime_taps_vs_oracle(S, O, fp, M, ntaps):
     """The headline kernel with the tap count at run time (any N <= 1024 at
-    M in 1/2/3/4/8/16, decim_stream_cf32<0, ...>): full chunks, the guarded
+    M in 1/2/3/4/6/8/12/16, decim_stream_cf32<0, ...>): full chunks, the guarded
     last chunk, taps past N never applied (inf / NaN samples in the stream and
     the history would turn a 0 * x into NaN), tail tiles and chained uneven
     calls, both float contracts."""
