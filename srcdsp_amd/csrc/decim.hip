@@ -111,10 +111,12 @@ int launch_ci16_dot2_shape(DecimLaunch L, int channels, bool mixed, hipStream_t 
         L.mix_pe_drow = (unsigned)((4ul * BLOCK) % L.mix_pe);
     }
     dim3 grid((unsigned)std::min<long>(L.ntiles, kCfGridCap * 256 / BLOCK), channels);
+    // M = 1 (16 outputs per lane) needs more than 128 VGPRs: 3 waves per SIMD
+    constexpr int MINW = MD == 1 ? 3 : 4;
     if (mixed)
-        hipLaunchKernelGGL((decim_dot2_ci16<NT, BLOCK, true, 4, TABM, MD>), grid, dim3(BLOCK), 0, s, L);
+        hipLaunchKernelGGL((decim_dot2_ci16<NT, BLOCK, true, MINW, TABM, MD>), grid, dim3(BLOCK), 0, s, L);
     else
-        hipLaunchKernelGGL((decim_dot2_ci16<NT, BLOCK, false, 4, 0, MD>), grid, dim3(BLOCK), 0, s, L);
+        hipLaunchKernelGGL((decim_dot2_ci16<NT, BLOCK, false, MINW, 0, MD>), grid, dim3(BLOCK), 0, s, L);
     return SRCDSP_OK;
 }
 
@@ -133,9 +135,10 @@ int launch_ci16_dot2(DecimLaunch L, int channels, bool mixed, hipStream_t s) {
     // reads for any frequency) when its period fits the LDS budget, else the
     // doubled phase table (only these instantiations are compiled outside the
     // tuning build)
+    constexpr int BLOCK = MD == 1 ? 256 : 512;  // M = 1: 3 workgroups of 4 waves per CU
     if (mixed && mixer_seq_period(L.mix_N, L.mix_freq) > kSeqMax)
-        return launch_ci16_dot2_shape<NT, 512, 1, MD>(L, channels, mixed, s);
-    return launch_ci16_dot2_shape<NT, 512, 2, MD>(L, channels, mixed, s);
+        return launch_ci16_dot2_shape<NT, BLOCK, 1, MD>(L, channels, mixed, s);
+    return launch_ci16_dot2_shape<NT, BLOCK, 2, MD>(L, channels, mixed, s);
 }
 
 template <int KV>
@@ -250,18 +253,21 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
         }
     } else if (f.M == 1 && f.kv == KV_F32_REAL && al && out_al && f.ntaps <= kFirMaxTaps && !mixed) {
         rc = launch_fir_tile<KV_F32_REAL>(L, channels, fma, s);
-    } else if ((f.M == 2 || f.M == 4 || f.M == 8 || f.M == 16) && f.kv == KV_CI16_I32 && f.coef_fits_i16 && al &&
-               out_al && f.ntaps <= kDot2MaxTaps) {
+    } else if ((f.M == 1 || f.M == 2 || f.M == 4 || f.M == 8 || f.M == 16) && f.kv == KV_CI16_I32 &&
+               f.coef_fits_i16 && al && out_al && f.ntaps <= kDot2MaxTaps) {
         // complex<int16_t> x int16-range taps on v_dot2 tap pairs, the mixer
         // fused when chained: at M = 4 the tap count compiled in at 127/128
         // (config 4) and, unmixed, 63/64/255/256; any other N <= kDot2MaxTaps
-        // and M = 2 / 8 / 16 at run time
+        // and M = 1 (FilterFir) / 2 / 8 / 16 at run time
         DecimLaunch L2 = L;
         L2.coef = f.d_cpair;
         if (f.M != 4) {
-            rc = f.M == 2 ? launch_ci16_dot2<0, 2>(L2, channels, mixed, s)
-                          : (f.M == 8 ? launch_ci16_dot2<0, 8>(L2, channels, mixed, s)
-                                      : launch_ci16_dot2<0, 16>(L2, channels, mixed, s));
+            switch (f.M) {
+            case 1: rc = launch_ci16_dot2<0, 1>(L2, channels, mixed, s); break;
+            case 2: rc = launch_ci16_dot2<0, 2>(L2, channels, mixed, s); break;
+            case 8: rc = launch_ci16_dot2<0, 8>(L2, channels, mixed, s); break;
+            default: rc = launch_ci16_dot2<0, 16>(L2, channels, mixed, s); break;
+            }
         } else if (f.ntaps == 127 || f.ntaps == 128) {
             rc = f.ntaps == 127 ? launch_ci16_dot2<127>(L2, channels, mixed, s) : launch_ci16_dot2<128>(L2, channels, mixed, s);
         } else if (!mixed && (f.ntaps == 63 || f.ntaps == 64 || f.ntaps == 255 || f.ntaps == 256)) {
@@ -292,7 +298,7 @@ int decim_launch(FirCore &f, const DecimLaunch &L, int channels, hipStream_t s, 
             rc = launch_decim_tile_m<KV_CI16_I32, 1>(L, channels, f.M, s);
     } else {
         if (mixed) {
-            set_error("mixer->decimator fusion needs variant 1, M = 2/4/8/16 with int16-range taps (N <= 1024) or M = 4 with "
+            set_error("mixer->decimator fusion needs variant 1, M = 1/2/4/8/16 with int16-range taps (N <= 1024) or M = 4 with "
                       "127/128 taps |c|<2^23, "
                       "16-B aligned input and output");
             return SRCDSP_ERR_UNSUPPORTED;

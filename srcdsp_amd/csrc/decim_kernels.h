@@ -1112,7 +1112,7 @@ __host__ __device__ constexpr int dot2_rt_halo(int ntaps) {
 }
 // device tap-pair array length: zero pairs of slack past the padded count for
 // the chunk of up to 24 pairs requested one chunk ahead
-constexpr int dot2_pair_slack = 32;
+constexpr int dot2_pair_slack = 32;  // >= the largest chunk (24 pairs at M = 1)
 __host__ __device__ constexpr int dot2_pair_alloc(int ntaps) { return dot2_rt_pairs(ntaps) + dot2_pair_slack; }
 __device__ __forceinline__ int32_t clamp_s14(int32_t v) {
     const int32_t a = v >> 14;  // |v| < 2^30: never INT_MIN
@@ -1362,7 +1362,7 @@ template <int NT, int BLOCK, bool MIX, int MINW, int TABM = 0, int MD = 4>
 __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     constexpr bool TAB2 = TABM == 1, SEQT = TABM == 2;
     constexpr bool RT = NT == 0;                  // the tap count at run time (a.ntaps <= kDot2MaxTaps)
-    static_assert(MD == 2 || MD == 4 || MD == 8 || MD == 16, "even M whose lane chunk is whole plane granules");
+    static_assert(MD == 1 || MD == 2 || MD == 4 || MD == 8 || MD == 16, "M dividing the 16-sample lane chunk");
     static_assert(MD == 4 || RT, "tap counts are compiled in at M = 4 only");
     constexpr int R = dot2_r(MD);                 // outputs per lane (a lane chunk: 16 samples)
     constexpr int TO = BLOCK * R;                 // outputs per tile
@@ -1593,10 +1593,23 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
         ConstPtr<uint32_t> tp = const_view<uint32_t>(a.coef);
         asm volatile("" : "+s"(tp));
         typedef uint32_t u4v_t __attribute__((ext_vector_type(4)));
-        int32_t yr[R], yi[R];
+        const unsigned sh = a.shift;
+        // limitScale16 of an accumulator pair (dnsampling_filters.h:167-168);
+        // Q14 taps: shift 14 (the common case), a saturating pack
+        auto quant = [&](auto &yr_, auto &yi_, uint32_t *w_, int n_, int stride_) {
+            if ((sh & 31u) != 0) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) yr[r] = yi[r] = 0;
+                for (int k = 0; k < n_; ++k) w_[k * stride_] = limit16_pair_sh(yr_[k], yi_[k], sh);
+            } else {
+#pragma unroll
+                for (int k = 0; k < n_; ++k) w_[k * stride_] = pack16(limit16(yr_[k], sh), limit16(yi_[k], sh));
+            }
+        };
+        uint32_t w[R];
         if constexpr (!RT) {
+            int32_t yr[R], yi[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) yr[r] = yi[r] = 0;
             // window: Dr[d + OFF], d in [-(4*NG), 8), NG = granules below the lane base
             constexpr int NG = ceildiv(JC - 1, 4);
             constexpr int OFF = 4 * NG;
@@ -1626,94 +1639,113 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
                     yi[r] = sdot2(Di[OFF + 2 * r - j], P, yi[r]);
                 }
             }
+            quant(yr, yi, w, R, 1);
         } else {
             // Run-time tap count: steps of 4 pairs.  Output r of a lane sits at
-            // dword r M/2 of the lane's plane chunk; pair j reads dword
-            // r M/2 - j, so step q (pairs 4q..4q+3) reads window granules
-            // -q-1 .. -q + EH/4 (EH = (R-1) M/2) and loads -q-2 for the next
-            // step: S = EH/4 + 3 register slots (granule c in slot c mod S)
-            // rotate with static names over chunks of U steps (an even
-            // multiple of S, so granule parity is static; 4U tap pairs,
-            // requested one chunk ahead).  A chunk starting at step q0 reads
-            // granule e - q0 at column t + (HG - q0)/2 + floor(e/2) of row
-            // e & 1: one base per chunk plus immediates.
-            constexpr int EH = (R - 1) * MD / 2;
-            constexpr int S = EH / 4 + 3;
-            constexpr int U = S % 2 ? 2 * S : S;
+            // sample r M of the lane chunk; pair j multiplies (x[rM - 2j],
+            // x[rM - 2j + 1]), i.e. plane dword rM/2 - j for even rM and, for
+            // odd rM (M = 1), the odd-aligned pair built from dwords a and a+1,
+            // a = (rM - 1)/2 - j, as (hi a, lo a+1) by one v_alignbit (reused
+            // over the step's outputs).  Step q (pairs 4q..4q+3) reads window
+            // granules -q-1 .. -q + EH/4 (EH = ceil((R-1) M/2)) and loads -q-2
+            // for the next step: S >= EH/4 + 3 register slots (granule c in
+            // slot c mod S, S even so granule parity is static) rotate with
+            // static names over chunks of S steps (4S tap pairs, requested one
+            // chunk ahead).  A chunk starting at step q0 reads granule e - q0
+            // at column t + (HG - q0)/2 + floor(e/2) of row e & 1: one base per
+            // chunk plus immediates.  At M = 1 (16 outputs per lane) the even
+            // and the odd outputs run as two passes over the taps, 8
+            // accumulator pairs each, in 256-lane workgroups at 3 waves per
+            // SIMD (one pass of 16 spilled even at that 168-VGPR budget).
+            constexpr int EH = ((R - 1) * MD + 1) / 2;
+            constexpr int S = EH / 4 + 3 + (EH / 4 + 3) % 2;
+            constexpr int U = S;
             constexpr int TPC = 4 * U;  // tap pairs per chunk
+            constexpr int RSTEP = MD == 1 ? 2 : 1, RP = R / RSTEP;  // output stride and count of a pass
             static_assert(TPC <= dot2_pair_slack, "the pair array's zero slack covers a chunk read ahead");
-            uint32_t W[S][2][4];  // [slot][plane][dword]
             auto slot = [](int e) { return ((e % S) + S) % S; };
-            auto load_e = [&](int cb, int e) {
-                const int o = cb + (e & 1) * NC + (e >> 1);
-                u4v_t gr = *(const u4v_t *)&lds[o];
-                u4v_t gi = *(const u4v_t *)&lds[o + 2 * NC];
-                asm volatile("" : "+v"(gr), "+v"(gi));  // whole ds_read_b128 (as above)
-                uint32_t(&w)[2][4] = W[slot(e)];
-                w[0][0] = gr[0]; w[0][1] = gr[1]; w[0][2] = gr[2]; w[0][3] = gr[3];
-                w[1][0] = gi[0]; w[1][1] = gi[1]; w[1][2] = gi[2]; w[1][3] = gi[3];
-            };
             auto chunk_base = [&](int q0) { return t + ((HG - q0) >> 1); };
             const int NS = J / 4;  // steps
-            // the lgkmcnt wait for a window read then never waits on a fresh s_load
-            uint32_t Tc[TPC], Tn[TPC];
-            auto load_taps = [&](uint32_t(&T)[TPC], int q0) {
-                ConstPtr<uint32_t> tc = tp + 4 * q0;
-                asm volatile("" : "+s"(tc));
+            auto pass = [&](auto r0_tag) {
+                constexpr int R0 = decltype(r0_tag)::value;  // first output of the pass
+                int32_t yr[RP], yi[RP];
 #pragma unroll
-                for (int i = 0; i < TPC; ++i) T[i] = tc[i];
-            };
-            load_taps(Tc, 0);
-            auto chunk = [&](int q0, auto steps_tag) {
-                constexpr int SN = decltype(steps_tag)::value;  // steps in this chunk (U, or a tail 1..U-1)
-                const int cb = chunk_base(q0);
+                for (int k = 0; k < RP; ++k) yr[k] = yi[k] = 0;
+                uint32_t W[S][2][4];  // [slot][plane][dword]
+                auto load_e = [&](int cb, int e) {
+                    const int o = cb + (e & 1) * NC + (e >> 1);
+                    u4v_t gr = *(const u4v_t *)&lds[o];
+                    u4v_t gi = *(const u4v_t *)&lds[o + 2 * NC];
+                    asm volatile("" : "+v"(gr), "+v"(gi));  // whole ds_read_b128 (as above)
+                    uint32_t(&ww)[2][4] = W[slot(e)];
+                    ww[0][0] = gr[0]; ww[0][1] = gr[1]; ww[0][2] = gr[2]; ww[0][3] = gr[3];
+                    ww[1][0] = gi[0]; ww[1][1] = gi[1]; ww[1][2] = gi[2]; ww[1][3] = gi[3];
+                };
+                // the lgkmcnt wait for a window read then never waits on a fresh s_load
+                uint32_t Tc[TPC], Tn[TPC];
+                auto load_taps = [&](uint32_t(&T)[TPC], int q0) {
+                    ConstPtr<uint32_t> tc = tp + 4 * q0;
+                    asm volatile("" : "+s"(tc));
 #pragma unroll
-                for (int s = 0; s < SN; ++s) {
-                    load_e(cb, -s - 2);
-                    if (SN == U && s == 0) load_taps(Tn, q0 + U);
+                    for (int i = 0; i < TPC; ++i) T[i] = tc[i];
+                };
+                load_taps(Tc, 0);
+                auto chunk = [&](int q0, auto steps_tag) {
+                    constexpr int SN = decltype(steps_tag)::value;  // steps in this chunk (U, or a tail 1..U-1)
+                    const int cb = chunk_base(q0);
 #pragma unroll
-                    for (int p = 0; p < 4; ++p) {
-                        const uint32_t P = Tc[4 * s + p];
+                    for (int s = 0; s < SN; ++s) {
+                        load_e(cb, -s - 2);
+                        if (SN == U && s == 0) load_taps(Tn, q0 + U);
 #pragma unroll
-                        for (int r = 0; r < R; ++r) {
-                            const int d = r * MD / 2 - 4 * s - p, e = floordiv(d, 4);
-                            yr[r] = sdot2(W[slot(e)][0][d - 4 * e], P, yr[r]);
-                            yi[r] = sdot2(W[slot(e)][1][d - 4 * e], P, yi[r]);
+                        for (int p = 0; p < 4; ++p) {
+                            const uint32_t P = Tc[4 * s + p];
+#pragma unroll
+                            for (int k = 0; k < RP; ++k) {
+                                const int r = R0 + k * RSTEP;
+                                auto dw = [&](int pl, int d) {
+                                    const int e = floordiv(d, 4);
+                                    return W[slot(e)][pl][d - 4 * e];
+                                };
+                                if ((r * MD) % 2 == 0) {
+                                    const int d = r * MD / 2 - 4 * s - p;
+                                    yr[k] = sdot2(dw(0, d), P, yr[k]);
+                                    yi[k] = sdot2(dw(1, d), P, yi[k]);
+                                } else {  // odd-aligned pair (x[2a+1], x[2a+2])
+                                    const int d = (r * MD - 1) / 2 - 4 * s - p;
+                                    yr[k] = sdot2(__builtin_amdgcn_alignbit(dw(0, d + 1), dw(0, d), 16), P, yr[k]);
+                                    yi[k] = sdot2(__builtin_amdgcn_alignbit(dw(1, d + 1), dw(1, d), 16), P, yi[k]);
+                                }
+                            }
                         }
                     }
-                }
-                if constexpr (SN == U) {
+                    if constexpr (SN == U) {
 #pragma unroll
-                    for (int i = 0; i < TPC; ++i) Tc[i] = Tn[i];
-                }
-            };
-            {
-                const int cb = chunk_base(0);
+                        for (int i = 0; i < TPC; ++i) Tc[i] = Tn[i];
+                    }
+                };
+                {
+                    const int cb = chunk_base(0);
 #pragma unroll
-                for (int e = EH / 4; e >= -1; --e) load_e(cb, e);
-            }
-            int q0 = 0;
-            for (; q0 + U <= NS; q0 += U) chunk(q0, std::integral_constant<int, U>{});
-            // the tail: 1 .. U-1 steps (wave-uniform), one unrolled body per length
-            auto tail = [&](auto self, auto k_tag) {
-                constexpr int K = decltype(k_tag)::value;
-                if constexpr (K < U) {
-                    if (NS - q0 == K) chunk(q0, k_tag);
-                    else self(self, std::integral_constant<int, K + 1>{});
+                    for (int e = EH / 4; e >= -1; --e) load_e(cb, e);
                 }
+                int q0 = 0;
+                for (; q0 + U <= NS; q0 += U) chunk(q0, std::integral_constant<int, U>{});
+                // the tail: 1 .. U-1 steps (wave-uniform), one unrolled body per length
+                auto tail = [&](auto self, auto k_tag) {
+                    constexpr int K = decltype(k_tag)::value;
+                    if constexpr (K < U) {
+                        if (NS - q0 == K) chunk(q0, k_tag);
+                        else self(self, std::integral_constant<int, K + 1>{});
+                    }
+                };
+                tail(tail, std::integral_constant<int, 1>{});
+                quant(yr, yi, w + R0, RP, RSTEP);
             };
-            tail(tail, std::integral_constant<int, 1>{});
+            pass(std::integral_constant<int, 0>{});
+            if constexpr (RSTEP == 2) pass(std::integral_constant<int, 1>{});
         }
         const long n0 = tile * TO + (long)t * R;
-        const unsigned sh = a.shift;
-        uint32_t w[R];
-        if ((sh & 31u) != 0) {  // Q14 taps: shift 14 (the common case)
-#pragma unroll
-            for (int r = 0; r < R; ++r) w[r] = limit16_pair_sh(yr[r], yi[r], sh);
-        } else {
-#pragma unroll
-            for (int r = 0; r < R; ++r) w[r] = pack16(limit16(yr[r], sh), limit16(yi[r], sh));
-        }
         if (n0 + R <= a.n_out) {
             if constexpr (R >= 4) {
 #pragma unroll

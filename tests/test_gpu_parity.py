@@ -215,13 +215,14 @@ DOT2_RT_TAPS = [1, 2, 3, 5, 17, 31, 62, 65, 100, 126, 129, 200, 257, 300, 511, 6
 DOT2_RT_SHAPES = ([(4, n) for n in DOT2_RT_TAPS] +
                   [(2, n) for n in (1, 2, 7, 31, 63, 64, 65, 127, 200, 1024)] +
                   [(8, n) for n in (1, 9, 63, 127, 128, 255, 300, 1024)] +
-                  [(16, n) for n in (1, 17, 127, 255, 256, 511, 1024)])
+                  [(16, n) for n in (1, 17, 127, 255, 256, 511, 1024)] +
+                  [(1, n) for n in (1, 2, 3, 16, 17, 31, 64, 127, 300, 1024)])
 
 
 @pytest.mark.parametrize("M,ntaps", DOT2_RT_SHAPES)
 def test_decim_ci16_dot2_runtime_taps_vs_oracle(S, O, M, ntaps):
     """The v_dot2 decimator with the tap count at run time (int16-range taps,
-    any N <= 1024 at M = 2, 8, 16, and at M = 4 off the compiled
+    any N <= 1024 at M = 1 (even / odd output passes), 2, 8, 16, and at M = 4 off the compiled
     63/64/127/128/255/256): the pairs padded with zero pairs to whole 4-pair
     steps, chunk tails, the longest halos; full-scale inputs (accumulator
     wrap, saturation), a call shorter than the filter, history carried over
@@ -242,11 +243,12 @@ def test_decim_ci16_dot2_runtime_taps_vs_oracle(S, O, M, ntaps):
                                          (4, 64, 4096, 0.5), (4, 129, 4096, 0.1), (4, 200, 3000, 0.3),
                                          (4, 255, 4093, 0.1), (4, 1024, 4096, 0.73), (2, 63, 4096, 0.1),
                                          (2, 127, 4093, -0.2), (8, 127, 4096, 0.1), (8, 255, 1000, 0.37),
-                                         (16, 255, 4096, 0.1), (16, 1024, 4093, 0.3)])
+                                         (16, 255, 4096, 0.1), (16, 1024, 4093, 0.3), (1, 31, 4096, 0.1),
+                                         (1, 128, 4093, -0.45)])
 def test_mixdecim_chain_runtime_taps(S, O, M, ntaps, N, f):
     """Config 4's fused mixer -> decimator off the compiled M = 4 x 127/128:
     the run-time-tap dot2 kernel with the mixer in its staging pass at
-    M = 2, 4, 8, 16, both mixer table forms (N = 4093 at f = 0.1 / -0.2 /
+    M = 1, 2, 4, 8, 16, both mixer table forms (N = 4093 at f = 0.1 / -0.2 /
     0.3: the doubled phase table), Q14 taps of the design filter and
     full-scale inputs; the same outputs and mixer state as the two
     reference calls."""
