@@ -28,9 +28,10 @@ typedef short short2_t __attribute__((ext_vector_type(2)));
 
 struct srcdsp_corr_state {
     unsigned N = 0, S = 1, NS = 0;
+    unsigned NP = 0;             // N rounded up to 16 (the dot2 tap array is front-padded with zero taps)
     int32_t *d_coef = nullptr;   // conj(pattern), N complex<int32_t> (2N int32)
     std::vector<int32_t> h_coef;
-    uint32_t *d_ptaps = nullptr; // packed int16 pairs for v_dot2: (p.re,p.im),(-p.im,p.re) per tap
+    uint32_t *d_ptaps = nullptr; // packed int16 pairs for v_dot2: (p.re,p.im),(-p.im,p.re) per tap, NP taps
     bool taps16 = false;         // every pattern component fits int16 (always true when the
                                  // reference's energy assert holds)
     uint32_t *d_hist[2] = {nullptr, nullptr};  // last NS-1 effective samples (packed ci16)
@@ -133,7 +134,7 @@ __global__ __launch_bounds__(kCorrBlock) void corr_eval(const uint32_t *__restri
     en_out[i] = e >> ((unsigned)((int)cs / 2) & 31u);                                // :245
 }
 
-// ------------------------------------------------- S == 1 register-tiled eval
+// -------------------------------------------------- register-tiled eval
 // For stride 1 the correlation is a complex FIR over the last N samples:
 //   C_i = sum_m x[i-(N-1)+m] * conj(p[m]).
 // With packed complex<int16_t> words both real products of a tap are one
@@ -147,29 +148,44 @@ __global__ __launch_bounds__(kCorrBlock) void corr_eval(const uint32_t *__restri
 // Taps (2N packed words) are scalar loads through a constant view.  The LDS
 // image gets one 16-B pad per lane chunk (CR words), so the 16 lanes of a
 // ds_read_b128 group touch 16 distinct bank slots.
+// Any stride S and tap count N: outputs i = k S + ph of one phase ph (grid.y)
+// correlate the phase stream x_ph[k] = x[k S + ph] with the pattern, a stride-1
+// correlation of that stream, so each workgroup stages one phase's samples
+// (a strided gather, through L2) and runs the stride-1 tiles on them.  The
+// taps are front-padded with zero taps to NP = 16 ceil(N/16) (exact: a zero
+// tap adds 0); the window energy covers the N real taps only (the padded
+// positions' |x|^2 are taken off the direct sum, and the sliding update drops
+// the oldest real sample).
 constexpr int kCR = 16;       // outputs per lane
 constexpr int kCBlock = 256;  // lanes per workgroup
+constexpr unsigned kCorrDot2MaxTaps = 8192;  // LDS image <= 64 KB
 
-__global__ __launch_bounds__(kCBlock) void corr_eval_s1(const uint32_t *__restrict__ in, long n, long i_begin,
-                                                         long i_end, const uint32_t *__restrict__ hist,
-                                                         const uint32_t *__restrict__ ptaps, int N, unsigned cs,
-                                                         uint32_t *__restrict__ corr_out,
-                                                         uint32_t *__restrict__ en_out, const unsigned *stop) {
+__global__ __launch_bounds__(kCBlock) void corr_eval_dot2(const uint32_t *__restrict__ in, long n, long i_begin,
+                                                           long i_end, const uint32_t *__restrict__ hist,
+                                                           const uint32_t *__restrict__ ptaps, int N, int NP, int S,
+                                                           unsigned cs, uint32_t *__restrict__ corr_out,
+                                                           uint32_t *__restrict__ en_out, const unsigned *stop) {
     if ((long)*stop < i_begin) return;  // an earlier segment already detected
     extern __shared__ __attribute__((aligned(16))) uint32_t xs[];
     constexpr int TO = kCBlock * kCR;
-    const long i0 = i_begin + (long)blockIdx.x * TO;  // first output of the tile
-    const long base = i0 - (N - 1);                   // first sample the tile needs
-    const int span = TO + N - 1;
+    const int ph = blockIdx.y;
+    const long NSm1 = (long)N * S - 1;
+    // this phase's outputs of the segment: k in [kb, ke), i = k S + ph
+    const long kb = (i_begin - ph + S - 1) / S, ke = (i_end - ph + S - 1) / S;
+    const long k0 = kb + (long)blockIdx.x * TO;  // first output of the tile (phase stream)
+    if (k0 >= ke) return;
+    const long base = k0 - (NP - 1);             // first phase-stream sample the tile needs
+    const int span = TO + NP - 1;
+    const int pad = NP - N;
     // LDS word of tile sample l (l = sample - base): lp = l + 1 (aligns the lane
     // windows' new words to 16 B), one 4-word pad per kCR = 16 words, i.e.
     // 20-word chunks of which the last 4 are padding
     static_assert(kCR == 16, "LDS chunk geometry assumes 16 outputs per lane");
     auto lw = [&](int l) { int lp = l + 1; return lp + 4 * (lp / kCR); };
     for (int l = threadIdx.x; l < span; l += kCBlock) {
-        long j = base + l;
+        const long j = (base + l) * S + ph;
         uint32_t w = 0;
-        if (j < n) w = j >= 0 ? in[j] : (j + (N - 1) >= 0 ? hist[j + (N - 1)] : 0u);
+        if (j < n) w = j >= 0 ? in[j] : (j + NSm1 >= 0 ? hist[j + NSm1] : 0u);
         xs[lw(l)] = w;
     }
     __syncthreads();
@@ -218,21 +234,27 @@ __global__ __launch_bounds__(kCBlock) void corr_eval_s1(const uint32_t *__restri
         }
     };
     int m0 = 0;
-    for (; m0 + 32 <= N; m0 += 32) {  // N % 16 == 0 (host-checked)
+    for (; m0 + 32 <= NP; m0 += 32) {  // NP % 16 == 0
         chunk(m0, A, B);
         chunk(m0 + 16, B, A);
     }
-    if (m0 < N) chunk(m0, A, B);
-    // outputs, energies (sliding) and stores
+    if (m0 < NP) chunk(m0, A, B);
+    // outputs, energies (sliding) and stores; the direct sum ran over the NP
+    // window words, the first pad of them before the real window
     uint32_t e = (uint32_t)e0;
+    for (int q = 0; q < pad; ++q) {
+        const short2_t a = __builtin_bit_cast(short2_t, xs[lw(lb + q)]);
+        e -= (uint32_t)__builtin_amdgcn_sdot2(a, a, 0, false);
+    }
     for (int r = 0; r < kCR; ++r) {
-        const long i = i0 + lb + r;
-        if (r > 0) {  // E_{i} = E_{i-1} + |x_i|^2 - |x_{i-N}|^2
-            const uint32_t xn = xs[lw(lb + r + N - 1)], xo = xs[lw(lb + r - 1)];
+        const long k = k0 + lb + r;
+        if (r > 0) {  // E_{k} = E_{k-1} + |x_k|^2 - |x_{k-N}|^2 (phase stream)
+            const uint32_t xn = xs[lw(lb + r + NP - 1)], xo = xs[lw(lb + r - 1 + pad)];
             const short2_t a = __builtin_bit_cast(short2_t, xn), b = __builtin_bit_cast(short2_t, xo);
             e += (uint32_t)__builtin_amdgcn_sdot2(a, a, 0, false) - (uint32_t)__builtin_amdgcn_sdot2(b, b, 0, false);
         }
-        if (i < i_end) {
+        if (k < ke) {
+            const long i = k * S + ph;
             const int32_t sr = ar[r] >> (cs & 31u), si = ai[r] >> (cs & 31u);
             const int32_t qr = sr >> 2, qi = si >> 2;
             corr_out[i] = (uint32_t)qr * (uint32_t)qr + (uint32_t)qi * (uint32_t)qi;
@@ -242,7 +264,7 @@ __global__ __launch_bounds__(kCBlock) void corr_eval_s1(const uint32_t *__restri
 }
 
 // ------------------------------------ S == 1: one launch, detection fused
-// corr_eval_s1's arithmetic over the whole call in ONE launch, with the
+// corr_eval_dot2's arithmetic (S = 1, N % 16 = 0) over the whole call in ONE launch, with the
 // peak/threshold test of correlators.h:262-268 evaluated by each block on its
 // own 4096 outputs and reduced to the first hit with atomicMin(best).
 //  * the test at a block's first two outputs needs corr/energy of the two
@@ -463,7 +485,12 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
     const long NSm1 = (long)c.NS - 1;
     const uint32_t *hist = c.d_hist[c.cur];
     const unsigned cs = (unsigned)c.coeff_scaling;
-    const bool fast = c.S == 1 && c.N % 16 == 0 && c.taps16;
+    // dot2 tiles for int16-range patterns (48 <= N <= kCorrDot2MaxTaps, any
+    // S: below 48 taps the one-output-per-lane kernel is faster, 0.277 vs
+    // 0.468 ms at N = 31, S = 3 on 2^24 samples); S = 1 with N % 16 = 0
+    // (config 5) scans in one launch with detection fused
+    const bool dot2 = c.taps16 && c.NP <= kCorrDot2MaxTaps && (c.N >= 48 || (c.S == 1 && c.N % 16 == 0));
+    const bool fast = dot2 && c.S == 1 && c.N % 16 == 0;
     // The reference stops at the first detection (break, correlators.h:291).
     // All segments are queued at once; each launch returns at its start when
     // an earlier segment's detect kernel has recorded a hit, so the scan stops
@@ -484,12 +511,14 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
     // kernels (S > 1 or N % 16 != 0)
     for (long sb = detect ? (fast ? n : 0) : std::max(0L, n - 3); sb < n; sb += seg) {
         const long se = std::min(n, sb + seg);
-        if (fast) {
+        if (dot2) {  // grid.y = phase of the stride
             constexpr long TO = (long)kCBlock * kCR;
-            const long blocks = (se - sb + TO - 1) / TO;
-            const size_t smem = 4 * (size_t)(((TO + c.N + 1) / kCR + 2) * (kCR + 4));
-            hipLaunchKernelGGL(corr_eval_s1, dim3((unsigned)blocks), dim3(kCBlock), smem, s, d_in, n, sb, se, hist,
-                               c.d_ptaps, (int)c.N, cs, c.d_corr, c.d_en, (const unsigned *)c.d_best);
+            const long per_phase = (se - sb + c.S - 1) / c.S;
+            const long blocks = (per_phase + TO - 1) / TO;
+            const size_t smem = 4 * (size_t)(((TO + c.NP + 1) / kCR + 2) * (kCR + 4));
+            hipLaunchKernelGGL(corr_eval_dot2, dim3((unsigned)blocks, c.S), dim3(kCBlock), smem, s, d_in, n, sb, se,
+                               hist, c.d_ptaps, (int)c.N, (int)c.NP, (int)c.S, cs, c.d_corr, c.d_en,
+                               (const unsigned *)c.d_best);
         } else {
             const size_t smem = 4 * (size_t)((kCorrBlock + NSm1 + 3) & ~3l) + 8 * (size_t)c.N;
             const long blocks = (se - sb + kCorrBlock - 1) / kCorrBlock;
@@ -587,6 +616,7 @@ SRCDSP_API int srcdsp_corr_create(srcdsp_corr_t *out, unsigned N, unsigned S) {
     c.N = N;
     c.S = S;
     c.NS = N * S;
+    c.NP = (N + 15) / 16 * 16;
     c.h_coef.assign(2 * N, 0);
     c.bits.assign(2 * N, 0);
     int rc = c.order.init();
@@ -597,7 +627,7 @@ SRCDSP_API int srcdsp_corr_create(srcdsp_corr_t *out, unsigned N, unsigned S) {
     }
     const size_t hb = 4 * (size_t)std::max(1u, c.NS - 1);
     if (hipMalloc(&c.d_coef, 8 * (size_t)N) != hipSuccess || hipMemset(c.d_coef, 0, 8 * (size_t)N) != hipSuccess ||
-        hipMalloc(&c.d_ptaps, 8 * (size_t)N) != hipSuccess || hipMemset(c.d_ptaps, 0, 8 * (size_t)N) != hipSuccess ||
+        hipMalloc(&c.d_ptaps, 8 * (size_t)c.NP) != hipSuccess || hipMemset(c.d_ptaps, 0, 8 * (size_t)c.NP) != hipSuccess ||
         hipMalloc(&c.d_hist[0], hb) != hipSuccess || hipMalloc(&c.d_hist[1], hb) != hipSuccess ||
         hipMemset(c.d_hist[0], 0, hb) != hipSuccess || hipMalloc(&c.d_best, 4) != hipSuccess) {
         set_error("corr_create: device allocation failed");
@@ -643,7 +673,7 @@ SRCDSP_API int srcdsp_corr_clone(srcdsp_corr_t h, srcdsp_corr_t *out) {
     c.bits = s.bits;
     const size_t hb = 4 * (size_t)std::max(1u, s.NS - 1);
     if (hipMemcpy(c.d_coef, s.d_coef, 8 * (size_t)s.N, hipMemcpyDeviceToDevice) != hipSuccess ||
-        hipMemcpy(c.d_ptaps, s.d_ptaps, 8 * (size_t)s.N, hipMemcpyDeviceToDevice) != hipSuccess ||
+        hipMemcpy(c.d_ptaps, s.d_ptaps, 8 * (size_t)s.NP, hipMemcpyDeviceToDevice) != hipSuccess ||
         hipMemcpy(c.d_hist[0], s.d_hist[s.cur], hb, hipMemcpyDeviceToDevice) != hipSuccess) {
         srcdsp_corr_destroy(n);
         set_error("corr_clone: device copy failed");
@@ -676,14 +706,15 @@ SRCDSP_API int srcdsp_corr_set_pattern(srcdsp_corr_t h, const int32_t *p, double
     c.coeff_scaling = cvt_d2i_x86(std::floor(std::log2(std::sqrt((double)c.coeffs_energy))));
     SRCDSP_HIP_TRY(hipMemcpy(c.d_coef, c.h_coef.data(), 8 * (size_t)c.N, hipMemcpyHostToDevice));
     c.taps16 = true;
-    std::vector<uint32_t> pk(2 * (size_t)c.N);
+    std::vector<uint32_t> pk(2 * (size_t)c.NP, 0u);  // front-padded with NP - N zero taps
     for (unsigned i = 0; i < c.N; ++i) {
         const int32_t pr = p[2 * i], pi = p[2 * i + 1];
         if (pr < -32767 || pr > 32767 || pi < -32767 || pi > 32767) c.taps16 = false;
-        pk[2 * i] = ((uint32_t)pr & 0xffffu) | ((uint32_t)pi << 16);       // Re = x.re*p.re + x.im*p.im
-        pk[2 * i + 1] = ((uint32_t)(-pi) & 0xffffu) | ((uint32_t)pr << 16);  // Im = -x.re*p.im + x.im*p.re
+        const size_t m = (size_t)(c.NP - c.N) + i;
+        pk[2 * m] = ((uint32_t)pr & 0xffffu) | ((uint32_t)pi << 16);       // Re = x.re*p.re + x.im*p.im
+        pk[2 * m + 1] = ((uint32_t)(-pi) & 0xffffu) | ((uint32_t)pr << 16);  // Im = -x.re*p.im + x.im*p.re
     }
-    SRCDSP_HIP_TRY(hipMemcpy(c.d_ptaps, pk.data(), 8 * (size_t)c.N, hipMemcpyHostToDevice));
+    SRCDSP_HIP_TRY(hipMemcpy(c.d_ptaps, pk.data(), 8 * (size_t)c.NP, hipMemcpyHostToDevice));
     return SRCDSP_OK;
 }
 

@@ -927,10 +927,16 @@ def test_offset_views_up_mixer_corr(S, O, in_off, out_off):
         assert np.array_equal(g.getRefBitSamples(), r.bit_samples())
 
 
-@pytest.mark.parametrize("N,S_", [(1024, 1), (32, 4), (64, 2)])
+@pytest.mark.parametrize("N,S_", [(1024, 1), (32, 4), (64, 2), (1, 1), (7, 5), (33, 1), (100, 1), (127, 2),
+                                  (31, 3), (16, 16), (1000, 1), (8200, 1), (48, 3), (50, 7), (256, 4)])
 def test_correlator_vs_oracle(S, O, N, S_):
+    """FixedPatternCorrelator at (N, S): the fused one-launch scan (S = 1,
+    N % 16 = 0), the dot2 tiles at any other N >= 48 and stride (the pattern
+    front-padded with zero taps to a multiple of 16, one phase of the stride
+    per grid row), and the generic kernel below 48 and past 8192 taps; stepping on after
+    every detection, bitSamples and registers compared at each."""
     from srcdsp_amd.design import qpsk_pattern
-    p = qpsk_pattern(N, 500, seed=N)
+    p = qpsk_pattern(N, 500 if N <= 2048 else 200, seed=N)
     rng = np.random.default_rng(N)
     n = 1 << 16 if N == 1024 else 1 << 17
     x = rng.integers(-125, 126, size=(n, 2)).astype(np.int32)
@@ -953,7 +959,9 @@ def test_correlator_vs_oracle(S, O, N, S_):
         assert all(st[k] == sr[k] for k in ("energy", "corr", "coeffs_energy", "coeff_scaling"))
         events += fr
         pos += (ir + 2) if fr else len(xs)
-    assert events >= 1
+    # these shapes' scaled statistics stay under the threshold for this
+    # signal (in the reference too): they check the registers at every step
+    assert events >= 1 or (N, S_) in {(1, 1), (7, 5), (16, 16), (48, 3), (50, 7)}
 
 
 def test_config5_size_properties(S, O):
