@@ -1,5 +1,7 @@
 """Kernel time of the v_dot2 interpolator (complex<int16_t>, int16-range taps)
-over phase lengths: 2^24 device-resident inputs, median of 50 launches."""
+over phase lengths: 2^24 device-resident inputs, median of 50 launches.
+
+  python scripts/up_envelope.py [L:ntaps ...]     (SRCDSP_HIP_LIB: another library build)"""
 import os
 import sys
 import numpy as np
@@ -11,7 +13,9 @@ from srcdsp_amd.design import hamming_sinc, q14
 n = 1 << 24
 x = torch.empty((n, 2), dtype=torch.int16, device="cuda")
 S.fill_synthetic(x, "ci16", seed=0x5EED, channel=0, lo=-8192, hi=8191)
-for L, ntaps in ((4, 64), (4, 128), (4, 256), (2, 32), (2, 64), (2, 128)):
+SHAPES = ((4, 64), (4, 128), (4, 256), (2, 32), (2, 64), (2, 128), (8, 128), (8, 256), (8, 512), (8, 1000))
+shapes = [tuple(int(v) for v in a.split(":")) for a in sys.argv[1:]] or SHAPES
+for L, ntaps in shapes:
     f = S.FilterUpsamplingFir(q14(hamming_sinc(ntaps, 0.12) * L), L)
     y = torch.empty((L * n, 2), dtype=torch.int16, device="cuda")
     for _ in range(10):

@@ -546,7 +546,7 @@ static int up_launch(srcdsp_up_state &u, const void *d_in, size_t n_in, void *d_
     void *hout0 = u.d_hist[u.cur ^ 1];
     const bool tiled = u.variant != UV_I16_I32 && (u.L == 2 || u.L == 4 || u.L == 8) && u.ntaps <= kUpMaxTaps &&
                        ((uintptr_t)d_in & 15u) == 0 && ((uintptr_t)d_out & 7u) == 0;
-    if (tiled && u.variant == UV_CI16_I32 && u.coef_i16 && (u.L == 2 || u.L == 4) &&
+    if (tiled && u.variant == UV_CI16_I32 && u.coef_i16 && (u.L == 2 || u.L == 4 || u.L == 8) &&
         ((uintptr_t)d_out & 15u) == 0) {
         constexpr int TI = kUpRD * kUpBlockD;
         const int PP = (u.H + 1) / 2, HG = (PP + 3) / 4, PGR = TI / 8 + HG;
@@ -570,13 +570,18 @@ static int up_launch(srcdsp_up_state &u, const void *d_in, size_t n_in, void *d_
         SRCDSP_UP_PP(4, 8)
         SRCDSP_UP_PP(4, 16)
         SRCDSP_UP_PP(4, 32)
+        SRCDSP_UP_PP(8, 8)
+        SRCDSP_UP_PP(8, 16)
 #undef SRCDSP_UP_PP
         if (u.L == 2) {
             constexpr int WSV = 3, MW = 1, PPV = 0;
             SRCDSP_UP_DOT2(2);
-        } else {
+        } else if (u.L == 4) {
             constexpr int WSV = 3, MW = 1, PPV = 0;
             SRCDSP_UP_DOT2(4);
+        } else {
+            constexpr int WSV = 3, MW = 1, PPV = 0;
+            SRCDSP_UP_DOT2(8);
         }
 #undef SRCDSP_UP_DOT2
         SRCDSP_HIP_TRY(hipGetLastError());
