@@ -546,7 +546,8 @@ static int up_launch(srcdsp_up_state &u, const void *d_in, size_t n_in, void *d_
     void *hout0 = u.d_hist[u.cur ^ 1];
     const bool tiled = u.variant != UV_I16_I32 && (u.L == 2 || u.L == 4 || u.L == 8) && u.ntaps <= kUpMaxTaps &&
                        ((uintptr_t)d_in & 15u) == 0 && ((uintptr_t)d_out & 7u) == 0;
-    if (tiled && u.variant == UV_CI16_I32 && u.coef_i16 && (u.L == 2 || u.L == 4 || u.L == 8) &&
+    const bool dot2_l = u.L >= 2 && u.L <= 8;  // up_tile_dot2: LR in 2..8
+    if (u.variant == UV_CI16_I32 && u.coef_i16 && dot2_l && u.ntaps <= kUpMaxTaps && ((uintptr_t)d_in & 15u) == 0 &&
         ((uintptr_t)d_out & 15u) == 0) {
         constexpr int TI = kUpRD * kUpBlockD;
         const int PP = (u.H + 1) / 2, HG = (PP + 3) / 4, PGR = TI / 8 + HG;
@@ -576,12 +577,16 @@ static int up_launch(srcdsp_up_state &u, const void *d_in, size_t n_in, void *d_
         if (u.L == 2) {
             constexpr int WSV = 3, MW = 1, PPV = 0;
             SRCDSP_UP_DOT2(2);
-        } else if (u.L == 4) {
-            constexpr int WSV = 3, MW = 1, PPV = 0;
-            SRCDSP_UP_DOT2(4);
         } else {
             constexpr int WSV = 3, MW = 1, PPV = 0;
-            SRCDSP_UP_DOT2(8);
+            switch (u.L) {
+            case 3: SRCDSP_UP_DOT2(3); break;
+            case 4: SRCDSP_UP_DOT2(4); break;
+            case 5: SRCDSP_UP_DOT2(5); break;
+            case 6: SRCDSP_UP_DOT2(6); break;
+            case 7: SRCDSP_UP_DOT2(7); break;
+            default: SRCDSP_UP_DOT2(8); break;
+            }
         }
 #undef SRCDSP_UP_DOT2
         SRCDSP_HIP_TRY(hipGetLastError());

@@ -860,10 +860,11 @@ def test_upsampler_tile_kernel_vs_oracle(S, O, variant, L, H):
 
 @pytest.mark.parametrize("L,H", [(2, 1), (2, 2), (2, 7), (2, 16), (2, 24), (2, 31), (2, 64), (4, 1), (4, 15), (4, 16),
                                  (4, 24), (4, 32), (4, 33), (4, 63), (4, 64), (4, 300), (8, 1), (8, 2), (8, 7),
-                                 (8, 15), (8, 16), (8, 17), (8, 32), (8, 33), (8, 100)])
+                                 (8, 15), (8, 16), (8, 17), (8, 32), (8, 33), (8, 100), (3, 1), (3, 16), (3, 33),
+                                 (5, 7), (5, 40), (6, 16), (7, 9), (7, 64)])
 def test_upsampler_dot2_kernel_vs_oracle(S, O, L, H):
     """<ci16,ci16,ci32,int32_t> with int16-range taps (incl. -32768, 32767) runs
-    the v_dot2 interpolator (L = 2, 4, 8); full-scale inputs so the int32
+    the v_dot2 interpolator (L = 2 .. 8); full-scale inputs so the int32
     accumulators wrap; flush and iterator overloads; uneven chained calls."""
     rng = np.random.default_rng(100 * L + H)
     c = rng.integers(-32768, 32768, size=L * H)
