@@ -207,3 +207,114 @@ def test_fuzz_correlator(S, O, seed):
         st = r.status()
         gs = g.getStatus()
         assert list(gs["corr"]) == st["corr"] and list(gs["energy"]) == st["energy"], (seed, op)
+
+
+# --- the run-time-shape kernels of round 3, drawn over their whole ranges ---
+# (decim_stream_cf32 / decim_dot2_ci16 at any N <= 1024 and M in {1, 2, 3, 4,
+# 6, 8, 12, 16}; up_tile_dot2 at L = 2..8 and any taps per phase;
+# corr_eval_dot2 at any N >= 48 and stride S; the fused chain at any N)
+
+def _any_taps(rng):
+    return int(rng.choice([int(rng.integers(2, 48)), int(rng.integers(48, 400)), int(rng.integers(400, 1025)),
+                           int(rng.integers(1025, 1300))]))
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_fuzz_decimator_any_shape(S, O, seed):
+    rng = np.random.default_rng(6000 + seed)
+    variant = int(rng.choice([0, 0, 1, 1, 2]))
+    M = int(rng.choice([1, 2, 3, 4, 6, 8, 12, 16]))
+    ntaps = _any_taps(rng)
+    fp = str(rng.choice(["fma", "strict"]))
+    c = _taps(rng, variant, ntaps)
+    if variant == 1 and rng.random() < 0.6:  # int16-range taps in an int32 filter: the dot2 kernel
+        c = rng.integers(-32768, 32768, ntaps).astype(np.int32)
+    g = S.FilterDnsamplingFir(c, M, *_DECIM_T[variant], fp=fp)
+    r = O[fp].decim(variant, M, c)
+    for op in range(6):
+        if rng.random() < 0.1:
+            g.reset()
+            r.reset()
+        n = M * int(rng.choice([0, 1, 5, 2047, 8193, int(rng.integers(0, 24000))]))
+        x = _input(rng, O, variant, n)
+        got, exp = _run(g, x, bool(rng.integers(0, 2))), r.step(x)
+        assert got.tobytes() == exp.tobytes(), (seed, op, variant, M, ntaps, fp, n)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_fuzz_upsampler_any_shape(S, O, seed):
+    rng = np.random.default_rng(7000 + seed)
+    L = int(rng.integers(2, 9))
+    H = int(rng.choice([int(rng.integers(1, 20)), int(rng.integers(20, 140))]))
+    c = rng.integers(-32767, 32768, L * H)
+    g = S.FilterUpsamplingFir(c, L, *_UP_T[0])
+    r = O["fma"].up(0, L, c)
+    for op in range(6):
+        if rng.random() < 0.1:
+            g.reset()
+            r.reset()
+        n = int(rng.choice([0, 1, 7, 2048, 4099, int(rng.integers(0, 12000))]))
+        x = O["fma"].gen_ci16(int(rng.integers(1 << 30)), 0, 0, n, -32768, 32767)
+        flush, it = bool(rng.random() < 0.2), bool(rng.random() < 0.3)
+        if bool(rng.integers(0, 2)):
+            got = g.step(_dev(x), None, flush, it).cpu().numpy()
+        else:
+            got = g.step(x, None, flush, it)
+        exp = r.step(x, flush, it)
+        assert got.tobytes() == exp.tobytes(), (seed, op, L, H, n, flush, it)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_fuzz_correlator_any_shape(S, O, seed):
+    from srcdsp_amd.design import qpsk_pattern
+    rng = np.random.default_rng(8000 + seed)
+    N, Sx = int(rng.integers(48, 330)), int(rng.integers(1, 6))
+    p = qpsk_pattern(N, int(rng.choice([200, 500])), seed=seed)
+    g, r = S.FixedPatternCorrelator(N, Sx), O["fma"].corr(N, Sx)
+    g.setPattern(p)
+    r.set_pattern(p)
+    for op in range(5):
+        if rng.random() < 0.1:
+            g.reset()
+            r.reset()
+        n = int(rng.choice([0, 1, 5, 9000, int(rng.integers(0, 40000))]))
+        x = rng.integers(-125, 126, size=(n, 2))
+        for _ in range(int(rng.integers(0, 3))):
+            if n > N * Sx + 10:
+                at = int(rng.integers(0, n - N * Sx))
+                x[at:at + N * Sx:Sx] += 2 * p
+        x = np.clip(x, -32768, 32767).astype(np.int16)
+        got = g.step(_dev(x)) if bool(rng.integers(0, 2)) else g.step(x)
+        exp = r.step(x)
+        assert got[0] == exp[0] and (not exp[0] or got[1] == exp[1]), (seed, op, N, Sx, n, got, exp)
+        if exp[0]:
+            assert np.array_equal(g.getRefBitSamples(), r.bit_samples())
+        st, gs = r.status(), g.getStatus()
+        assert list(gs["corr"]) == st["corr"] and list(gs["energy"]) == st["energy"], (seed, op, N, Sx)
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_fuzz_chain_any_shape(S, O, seed):
+    rng = np.random.default_rng(9000 + seed)
+    N = int(rng.choice([16, 1000, 4096]))
+    f = float(rng.uniform(-1, 1))
+    m, om = S.Mixer(N), O["fma"].mixer(N)
+    m.reset(f)
+    om.reset(f)
+    Md = int(rng.choice([1, 2, 4, 8, 16]))
+    nt = int(rng.integers(2, 1025))
+    c = rng.integers(-32768, 32768, nt).astype(np.int32)
+    d = S.FilterDnsamplingFir(c, Md, *_DECIM_T[1])
+    chain = S.MixerDecimatorChain(m, d)
+    od = O["fma"].decim(1, Md, c)
+    for op in range(6):
+        if rng.random() < 0.15:
+            a = float(rng.uniform(-0.5, 0.5))
+            m.adjustFrequency(a)
+            om.adjust_frequency(a)
+        n = 16 * int(rng.choice([0, 1, 7, 1000, int(rng.integers(0, 12000))]))
+        x = O["fma"].gen_ci16(int(rng.integers(1 << 30)), 0, 0, n, -32768, 32767)
+        got = chain.step(_dev(x)).cpu().numpy()
+        exp = od.step(om.step(x))
+        assert got.tobytes() == exp.tobytes(), (seed, op, N, Md, nt, n)
+        assert m.state()[:2] == om.state()[:2]
