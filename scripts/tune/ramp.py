@@ -6,7 +6,9 @@
 
 VARIANT: a tune_decim id (70 = the product headline shape, 71 = its memory
 path only, 73 = its compute path only on L2-resident input), "prod" (the
-product library's FilterDnsamplingFir.step), "w:<workload>" (one step of a
+product library's FilterDnsamplingFir.step), "prodT<n>" (the same at M = 4
+with an n-tap filter: the tap loop's share of the energy varies, the bytes do
+not), "w:<workload>" (one step of a
 bench.py workload: w:mixdecim, w:ci16decim, w:up, w:corr, w:fir), "read"
 (read-only stream) or "copy" (4:1 coalesced stream).  A one-lane clock probe runs on a second
 stream for the whole run; every launch's kernel time is printed with the mean
@@ -72,6 +74,7 @@ def main():
             spec.loader.exec_module(bench)
             n_w = (1 << 26) if v[2:] in ("corr", "up") else (1 << 28)
             works[v] = bench.WORKLOADS[v[2:]](S, torch, n_w, 1, 0, "fma")
+    fT = {v: S.FilterDnsamplingFir(hamming_sinc(int(v[5:])), 4) for v in set(seq) if v.startswith("prodT")}
     torch.cuda.synchronize()
 
     def launch(var):
@@ -79,6 +82,8 @@ def main():
             works[var].step()
         elif var == "prod":
             f.step(x, y)
+        elif var in fT:
+            fT[var].step(x, y)
         elif var == "read":
             lib.tune_stream_probe2(1, 8192, C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), L, st)
         elif var == "copy":
