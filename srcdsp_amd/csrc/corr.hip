@@ -95,6 +95,8 @@ __device__ __forceinline__ uint32_t corr_fetch(const uint32_t *in, const uint32_
 }
 
 constexpr int kCorrBlock = 256;
+constexpr size_t kCorrEvalMaxSmem = 64 * 1024;  // corr_eval's staged window + taps; longer: corr_eval_g
+constexpr unsigned kCorrMaxGridY = 65535;       // corr_eval_dot2 runs one stride phase per grid row
 
 // one output per lane; the block's window span and the taps are staged in LDS
 __global__ __launch_bounds__(kCorrBlock) void corr_eval(const uint32_t *__restrict__ in, long n, long i_begin,
@@ -159,6 +161,36 @@ __global__ __launch_bounds__(kCorrBlock) void corr_eval(const uint32_t *__restri
 constexpr int kCR = 16;       // outputs per lane
 constexpr int kCBlock = 256;  // lanes per workgroup
 constexpr unsigned kCorrDot2MaxTaps = 8192;  // LDS image <= 64 KB
+
+// corr_eval's arithmetic for windows too long to stage (N*S + 255 samples
+// past kCorrEvalMaxSmem of LDS, e.g. S in the thousands): one output per lane,
+// window samples and taps read through the cache (adjacent lanes read
+// adjacent samples, so every tap is one coalesced load per wave)
+__global__ __launch_bounds__(kCorrBlock) void corr_eval_g(const uint32_t *__restrict__ in, long n, long i_begin,
+                                                          long i_end, const uint32_t *__restrict__ hist,
+                                                          const int32_t *__restrict__ coef, unsigned N, unsigned S,
+                                                          unsigned cs, uint32_t *__restrict__ corr_out,
+                                                          uint32_t *__restrict__ en_out, const unsigned *stop) {
+    if ((long)*stop < i_begin) return;
+    const long i = i_begin + (long)blockIdx.x * kCorrBlock + threadIdx.x;
+    if (i >= i_end) return;
+    const long NSm1 = (long)N * S - 1;
+    uint32_t tr = 0, ti = 0, e = 0;
+    // tap m multiplies x[i - (N-1-m) S]
+    long j = i - (long)(N - 1) * S;
+    for (unsigned m = 0; m < N; ++m, j += S) {
+        const uint32_t w = j < n ? corr_fetch(in, hist, j, NSm1) : 0u;
+        const int32_t hr = sext16(w), hi = sext16_hi(w);
+        const int32_t cr = coef[2 * m], ci = coef[2 * m + 1];
+        tr += (uint32_t)hr * (uint32_t)cr - (uint32_t)hi * (uint32_t)ci;
+        ti += (uint32_t)hr * (uint32_t)ci + (uint32_t)hi * (uint32_t)cr;
+        e += (uint32_t)hr * (uint32_t)hr + (uint32_t)hi * (uint32_t)hi;
+    }
+    const int32_t sr = (int32_t)tr >> (cs & 31u), si = (int32_t)ti >> (cs & 31u);  // scale32 :244
+    const int32_t ar = sr >> 2, ai = si >> 2;                                       // :250
+    corr_out[i] = (uint32_t)ar * (uint32_t)ar + (uint32_t)ai * (uint32_t)ai;
+    en_out[i] = e >> ((unsigned)((int)cs / 2) & 31u);                                // :245
+}
 
 __global__ __launch_bounds__(kCBlock) void corr_eval_dot2(const uint32_t *__restrict__ in, long n, long i_begin,
                                                            long i_end, const uint32_t *__restrict__ hist,
@@ -489,7 +521,8 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
     // S: below 48 taps the one-output-per-lane kernel is faster, 0.277 vs
     // 0.468 ms at N = 31, S = 3 on 2^24 samples); S = 1 with N % 16 = 0
     // (config 5) scans in one launch with detection fused
-    const bool dot2 = c.taps16 && c.NP <= kCorrDot2MaxTaps && (c.N >= 48 || (c.S == 1 && c.N % 16 == 0));
+    const bool dot2 = c.taps16 && c.NP <= kCorrDot2MaxTaps && c.S <= kCorrMaxGridY &&
+                      (c.N >= 48 || (c.S == 1 && c.N % 16 == 0));
     const bool fast = dot2 && c.S == 1 && c.N % 16 == 0;
     // The reference stops at the first detection (break, correlators.h:291).
     // All segments are queued at once; each launch returns at its start when
@@ -522,8 +555,12 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
         } else {
             const size_t smem = 4 * (size_t)((kCorrBlock + NSm1 + 3) & ~3l) + 8 * (size_t)c.N;
             const long blocks = (se - sb + kCorrBlock - 1) / kCorrBlock;
-            hipLaunchKernelGGL(corr_eval, dim3((unsigned)blocks), dim3(kCorrBlock), smem, s, d_in, n, sb, se, hist,
-                               c.d_coef, c.N, c.S, cs, c.d_corr, c.d_en, (const unsigned *)c.d_best);
+            if (smem <= kCorrEvalMaxSmem)
+                hipLaunchKernelGGL(corr_eval, dim3((unsigned)blocks), dim3(kCorrBlock), smem, s, d_in, n, sb, se, hist,
+                                   c.d_coef, c.N, c.S, cs, c.d_corr, c.d_en, (const unsigned *)c.d_best);
+            else
+                hipLaunchKernelGGL(corr_eval_g, dim3((unsigned)blocks), dim3(kCorrBlock), 0, s, d_in, n, sb, se, hist,
+                                   c.d_coef, c.N, c.S, cs, c.d_corr, c.d_en, (const unsigned *)c.d_best);
         }
         SRCDSP_HIP_TRY(hipGetLastError());
         if (!detect) continue;

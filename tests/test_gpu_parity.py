@@ -966,6 +966,38 @@ def test_correlator_vs_oracle(S, O, N, S_):
     assert events >= 1 or (N, S_) in {(1, 1), (7, 5), (16, 16), (48, 3), (50, 7)}
 
 
+@pytest.mark.parametrize("N,S_,n,chunk", [(32, 2100, 1 << 18, 50000), (64, 70000, 5_500_000, 1_000_000),
+                                           (64, 600, 1 << 18, 70000)])
+def test_correlator_long_window_vs_oracle(S, O, N, S_, n, chunk):
+    """Windows N*S too long to stage in LDS (corr_eval_g: one output per lane
+    through the cache) and strides past one grid row per phase (S > 65535 leaves
+    the dot2 tiles); (64, 600) is the dot2 tile kernel at a long stride.  Bytes,
+    detections, bitSamples and registers against the oracle at every step."""
+    from srcdsp_amd.design import qpsk_pattern
+    p = qpsk_pattern(N, 500, seed=N)
+    rng = np.random.default_rng(N + S_)
+    x = rng.integers(-125, 126, size=(n, 2)).astype(np.int32)
+    off = n - N * S_ - 1000
+    for m in range(N):
+        x[off + m * S_] += 2 * p[m]
+    x = np.clip(x, -32768, 32767).astype(np.int16)
+    g, r = S.FixedPatternCorrelator(N, S_), O["fma"].corr(N, S_)
+    g.setPattern(p)
+    r.set_pattern(p)
+    pos, events = 0, 0
+    while pos < n:
+        xs = x[pos:pos + chunk]
+        fg, ig = g.step(dev(xs))
+        fr, ir = r.step(xs)
+        assert (fg, fg and ig) == (fr, fr and ir)
+        assert np.array_equal(g.getRefBitSamples(), r.bit_samples())
+        st, sr = g.getStatus(), r.status()
+        assert all(st[k] == sr[k] for k in ("energy", "corr", "coeffs_energy", "coeff_scaling"))
+        events += fr
+        pos += (ir + 2) if fr else len(xs)
+    assert events >= 1
+
+
 def test_config5_size_properties(S, O):
     """Config 5 at full size (2^26 samples, device-resident, one step): the
     bench's buffer (noise +-125, the 1024-sample QPSK pattern x2 at 3/4).  The
