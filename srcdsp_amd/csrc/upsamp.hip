@@ -65,13 +65,18 @@ __device__ __forceinline__ uint32_t up_fetch(const void *in, const void *hist, l
     return UV == UV_I16_I32 ? (uint32_t)(uint16_t)((const int16_t *)in)[j] : ((const uint32_t *)in)[j];
 }
 
-template <int UV>
+template <int UV, bool LDS = true>
 __global__ __launch_bounds__(256) void up_kernel(const void *in, long n_in, long n_total, const void *hist_in,
                                                  void *hist_out, const int32_t *coef, int H, unsigned L,
                                                  unsigned shift, void *out) {
-    extern __shared__ int32_t sc[];  // L*H polyphase taps
-    for (int i = threadIdx.x; i < (int)(L * H); i += blockDim.x) sc[i] = coef[i];
-    __syncthreads();
+    // L*H polyphase taps: staged in LDS, or (!LDS: past kUpKernelMaxSmem) read
+    // through the cache, wave-uniform
+    extern __shared__ int32_t sc_lds[];
+    if constexpr (LDS) {
+        for (int i = threadIdx.x; i < (int)(L * H); i += blockDim.x) sc_lds[i] = coef[i];
+        __syncthreads();
+    }
+    const int32_t *sc = LDS ? sc_lds : coef;
     const int Hm1 = H - 1;
     if (blockIdx.x == 0) {  // new history: last H-1 samples of the virtual stream
         for (int k = threadIdx.x; k < Hm1; k += blockDim.x) {
@@ -105,6 +110,7 @@ __global__ __launch_bounds__(256) void up_kernel(const void *in, long n_in, long
 // has checked |c| < 2^23 (I24), exact 32-bit multiply otherwise; the int16
 // variant wraps each product to int16 (std::operator*, UV_CI16_I16).
 constexpr int kUpR = 4, kUpBlock = 256, kUpMaxTaps = 4096;
+constexpr size_t kUpKernelMaxSmem = 64 * 1024;  // up_kernel's taps in LDS; longer filters read them through the cache
 
 template <int UV, int LR, bool I24>
 __global__ __launch_bounds__(kUpBlock) void up_tile(const uint32_t *in, long n_in, long n_total,
@@ -627,20 +633,19 @@ static int up_launch(srcdsp_up_state &u, const void *d_in, size_t n_in, void *d_
     const size_t smem = 4 * (size_t)u.ntaps;
     const void *hin = u.d_hist[u.cur];
     void *hout = u.d_hist[u.cur ^ 1];
+#define SRCDSP_UP_GENERIC(UVV)                                                                                      \
+    if (smem <= kUpKernelMaxSmem)                                                                                   \
+        hipLaunchKernelGGL((up_kernel<UVV, true>), dim3(blocks), dim3(256), smem, s, d_in, (long)n_in, n_total, hin, \
+                           hout, u.d_coef, u.H, u.L, shift, d_out);                                                \
+    else                                                                                                            \
+        hipLaunchKernelGGL((up_kernel<UVV, false>), dim3(blocks), dim3(256), 0, s, d_in, (long)n_in, n_total, hin,  \
+                           hout, u.d_coef, u.H, u.L, shift, d_out);
     switch (u.variant) {
-    case UV_CI16_I32:
-        hipLaunchKernelGGL(up_kernel<UV_CI16_I32>, dim3(blocks), dim3(256), smem, s, d_in, (long)n_in, n_total, hin,
-                           hout, u.d_coef, u.H, u.L, shift, d_out);
-        break;
-    case UV_CI16_I16:
-        hipLaunchKernelGGL(up_kernel<UV_CI16_I16>, dim3(blocks), dim3(256), smem, s, d_in, (long)n_in, n_total, hin,
-                           hout, u.d_coef, u.H, u.L, shift, d_out);
-        break;
-    default:
-        hipLaunchKernelGGL(up_kernel<UV_I16_I32>, dim3(blocks), dim3(256), smem, s, d_in, (long)n_in, n_total, hin,
-                           hout, u.d_coef, u.H, u.L, shift, d_out);
-        break;
+    case UV_CI16_I32: SRCDSP_UP_GENERIC(UV_CI16_I32) break;
+    case UV_CI16_I16: SRCDSP_UP_GENERIC(UV_CI16_I16) break;
+    default: SRCDSP_UP_GENERIC(UV_I16_I32) break;
     }
+#undef SRCDSP_UP_GENERIC
     SRCDSP_HIP_TRY(hipGetLastError());
     u.cur ^= 1;
     return u.order.after(s);

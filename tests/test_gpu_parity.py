@@ -833,10 +833,11 @@ _UP_TYPES = {0: ("complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "in
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2])
-@pytest.mark.parametrize("L,H", [(2, 1), (2, 7), (4, 32), (4, 33), (8, 16), (3, 5), (4, 2000)])
+@pytest.mark.parametrize("L,H", [(2, 1), (2, 7), (4, 32), (4, 33), (8, 16), (3, 5), (4, 2000), (3, 6000), (16, 1100)])
 def test_upsampler_tile_kernel_vs_oracle(S, O, variant, L, H):
     """Tiled interpolator (L in 2/4/8, <= 4096 taps) and the generic one (other
-    L, int16 input, longer filters): flush and iterator overloads, wide taps
+    L, int16 input, longer filters; past 16384 taps it reads them through the
+    cache): flush and iterator overloads, wide taps
     (|c| >= 2^23 takes the exact 32-bit multiply), int16 product wrap."""
     rng = np.random.default_rng(L * 1000 + H + 7 * variant)
     n = L * H
