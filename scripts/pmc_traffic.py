@@ -23,7 +23,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from srcdsp_amd.build import source_digest  # noqa: E402
-KERNEL_KEYS = {"decim": "decim_stream_cf32", "mixdecim": "decim_dot2_ci16", "ci16decim": "decim_dot2_ci16", "corr": "corr_eval",
+KERNEL_KEYS = {"decim": "decim_stream_cf32", "mixdecim": "decim_dot2_ci16", "ci16decim": "decim_dot2_ci16", "corr": "corr_scan_s1",
                "fir": "fir_stream_f32", "up": "up_tile"}
 BYTES_PER_SAMPLE = {"decim": 10.0, "mixdecim": 5.0, "ci16decim": 5.0, "corr": 4.0, "fir": 12.0, "up": 20.0}
 NAMES = {"decim": "decim_cf32_m4_t127", "mixdecim": "mixer4096_f0.1_to_decim_ci16_q14_m4_t127",
@@ -61,9 +61,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="decim")
     ap.add_argument("--tag", default="latest")
-    ap.add_argument("--samples", type=int, default=1 << 28)
+    ap.add_argument("--samples", type=int, default=None, help="default: bench.py's (2^28; corr: 2^26, config 5)")
     ap.add_argument("--channels", type=int, default=1, help="decim only: channels per launch (config 3's share: 8)")
     a = ap.parse_args()
+    if a.samples is None:
+        a.samples = (1 << 26) if a.workload == "corr" else (1 << 28)
     key = KERNEL_KEYS[a.workload]
     steps_run = 6  # bench.py --warmup 1 --steps 5: every step's dispatches are counted
     bench_args = ["--workload", a.workload, "--steps", "5", "--warmup", "1", "--no-cpu-baseline", "--no-pcie",

@@ -454,8 +454,10 @@ __global__ __launch_bounds__(kCBlock) void corr_scan_s1(const uint32_t *__restri
     for (int r = 0; r < kCR; ++r) {
         const long i = i0 + lb + r;
         if (i < n) {
-            corr_out[i] = cv[r];
-            en_out[i] = ev[r];
+            if (corr_out) {  // (the product passes none: corr_point recomputes what the registers need)
+                corr_out[i] = cv[r];
+                en_out[i] = ev[r];
+            }
             const uint32_t c1 = r >= 1 ? cv[r - 1] : cm1;
             const uint32_t c2 = r >= 2 ? cv[r - 2] : (r == 1 ? cm1 : cm2);
             const uint32_t e1 = r >= 1 ? ev[r - 1] : em1;
@@ -487,6 +489,51 @@ __global__ void corr_history(const uint32_t *in, const uint32_t *hist_in, uint32
         hist_out[k] = corr_fetch(in, hist_in, last - NSm1 + 1 + k, NSm1);
 }
 
+// The registers after a fused scan (corr_scan_s1 stores no per-sample values):
+// corr and energy at last-2 .. last, last = the detected sample (*best) or
+// n - 1, each a direct sum over the N taps with corr_eval's arithmetic
+// (int32 wrap-around sums, so equal to the scan's sliding energy).  One block;
+// out[k] = corr(last - k), out[3 + k] = energy(last - k) for last - k >= 0.
+__global__ __launch_bounds__(256) void corr_point(const uint32_t *__restrict__ in, long n,
+                                                  const uint32_t *__restrict__ hist,
+                                                  const int32_t *__restrict__ coef, unsigned N, unsigned S, unsigned cs,
+                                                  const unsigned *__restrict__ best, uint32_t *__restrict__ out) {
+    __shared__ uint32_t red[3][3][256];
+    const unsigned b = *best;
+    const long last = b != 0xffffffffu ? (long)b : n - 1;
+    const long NSm1 = (long)N * S - 1;
+    for (int k = 0; k < 3; ++k) {
+        uint32_t tr = 0, ti = 0, e = 0;
+        const long i = last - k;
+        if (i >= 0)
+            for (unsigned m = threadIdx.x; m < N; m += blockDim.x) {
+                const uint32_t w = corr_fetch(in, hist, i - (long)(N - 1 - m) * S, NSm1);
+                const int32_t hr = sext16(w), hi = sext16_hi(w);
+                const int32_t cr = coef[2 * m], ci = coef[2 * m + 1];
+                tr += (uint32_t)hr * (uint32_t)cr - (uint32_t)hi * (uint32_t)ci;
+                ti += (uint32_t)hr * (uint32_t)ci + (uint32_t)hi * (uint32_t)cr;
+                e += (uint32_t)hr * (uint32_t)hr + (uint32_t)hi * (uint32_t)hi;
+            }
+        red[k][0][threadIdx.x] = tr;
+        red[k][1][threadIdx.x] = ti;
+        red[k][2][threadIdx.x] = e;
+    }
+    __syncthreads();
+    for (int w = 128; w >= 1; w >>= 1) {
+        if ((int)threadIdx.x < w)
+            for (int k = 0; k < 3; ++k)
+                for (int q = 0; q < 3; ++q) red[k][q][threadIdx.x] += red[k][q][threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x < 3) {
+        const int k = threadIdx.x;
+        const int32_t sr = (int32_t)red[k][0][0] >> (cs & 31u), si = (int32_t)red[k][1][0] >> (cs & 31u);
+        const int32_t ar = sr >> 2, ai = si >> 2;
+        out[k] = (uint32_t)ar * (uint32_t)ar + (uint32_t)ai * (uint32_t)ai;
+        out[3 + k] = red[k][2][0] >> ((unsigned)((int)cs / 2) & 31u);
+    }
+}
+
 // ---------------------------------------------------------------- host side
 static int corr_alloc_scratch(srcdsp_corr_state &c, size_t n) {
     if (n <= c.scratch_cap) return SRCDSP_OK;
@@ -512,8 +559,6 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
     }
     int rc = c.order.before(s);
     if (rc) return rc;
-    rc = corr_alloc_scratch(c, n_);
-    if (rc) return rc;
     const long NSm1 = (long)c.NS - 1;
     const uint32_t *hist = c.d_hist[c.cur];
     const unsigned cs = (unsigned)c.coeff_scaling;
@@ -524,6 +569,14 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
     const bool dot2 = c.taps16 && c.NP <= kCorrDot2MaxTaps && c.S <= kCorrMaxGridY &&
                       (c.N >= 48 || (c.S == 1 && c.N % 16 == 0));
     const bool fast = dot2 && c.S == 1 && c.N % 16 == 0;
+    // the fused scan keeps no per-sample values (corr_point computes the three
+    // the registers need); the segmented kernels write corr/energy per sample
+    // for corr_detect
+    const bool fused = fast && detect;
+    if (!fused) {
+        rc = corr_alloc_scratch(c, n_);
+        if (rc) return rc;
+    }
     // The reference stops at the first detection (break, correlators.h:291).
     // All segments are queued at once; each launch returns at its start when
     // an earlier segment's detect kernel has recorded a hit, so the scan stops
@@ -532,12 +585,15 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
     const unsigned none = 0xffffffffu;
     unsigned best = none;
     SRCDSP_HIP_TRY(hipMemsetAsync(c.d_best, 0xff, 4, s));
-    if (fast && detect) {  // one launch, detection fused, in-flight early exit
+    if (fused) {  // one launch, detection fused, in-flight early exit
         constexpr long TO = (long)kCBlock * kCR;
         const long blocks = (n + TO - 1) / TO;
         const size_t smem = 4 * (size_t)(((TO + c.N + 1) / kCR + 2) * (kCR + 4));
         hipLaunchKernelGGL(corr_scan_s1, dim3((unsigned)blocks), dim3(kCBlock), smem, s, d_in, n, hist, c.d_ptaps,
-                           (int)c.N, cs, c.corr[0], c.corr[1], c.energy[0], c.d_corr, c.d_en, c.d_best);
+                           (int)c.N, cs, c.corr[0], c.corr[1], c.energy[0], nullptr, nullptr, c.d_best);
+        SRCDSP_HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(corr_point, dim3(1), dim3(256), 0, s, d_in, n, hist, c.d_coef, c.N, c.S, cs,
+                           (const unsigned *)c.d_best, c.d_best + 2);
         SRCDSP_HIP_TRY(hipGetLastError());
     }
     // the segmented path: priming (the last 3 positions only) and the generic
@@ -569,8 +625,10 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
                            c.energy[0], c.d_best);
         SRCDSP_HIP_TRY(hipGetLastError());
     }
-    SRCDSP_HIP_TRY(hipMemcpyAsync(&best, c.d_best, 4, hipMemcpyDeviceToHost, s));
+    unsigned words[8];  // best, pad, corr_point's corr[3] and energy[3]
+    SRCDSP_HIP_TRY(hipMemcpyAsync(words, c.d_best, fused ? sizeof words : 4, hipMemcpyDeviceToHost, s));
     SRCDSP_HIP_TRY(hipStreamSynchronize(s));
+    best = words[0];
 
     const bool hit = best != none;
     const long last = hit ? (long)best : n - 1;  // last processed sample
@@ -578,8 +636,15 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
     uint32_t cw[3] = {0, 0, 0}, ew[3] = {0, 0, 0};
     const long lo = std::max(0L, last - 2);
     const long cnt = last - lo + 1;
-    SRCDSP_HIP_TRY(hipMemcpy(cw, c.d_corr + lo, 4 * cnt, hipMemcpyDeviceToHost));
-    SRCDSP_HIP_TRY(hipMemcpy(ew, c.d_en + lo, 4 * cnt, hipMemcpyDeviceToHost));
+    if (fused) {
+        for (long idx = lo; idx <= last; ++idx) {
+            cw[idx - lo] = words[2 + (last - idx)];
+            ew[idx - lo] = words[5 + (last - idx)];
+        }
+    } else {
+        SRCDSP_HIP_TRY(hipMemcpy(cw, c.d_corr + lo, 4 * cnt, hipMemcpyDeviceToHost));
+        SRCDSP_HIP_TRY(hipMemcpy(ew, c.d_en + lo, 4 * cnt, hipMemcpyDeviceToHost));
+    }
     uint32_t nc[3], ne[3];
     for (int k = 0; k < 3; ++k) {  // nc[k] = corr of sample last-k
         long idx = last - k;
@@ -666,7 +731,7 @@ SRCDSP_API int srcdsp_corr_create(srcdsp_corr_t *out, unsigned N, unsigned S) {
     if (hipMalloc(&c.d_coef, 8 * (size_t)N) != hipSuccess || hipMemset(c.d_coef, 0, 8 * (size_t)N) != hipSuccess ||
         hipMalloc(&c.d_ptaps, 8 * (size_t)c.NP) != hipSuccess || hipMemset(c.d_ptaps, 0, 8 * (size_t)c.NP) != hipSuccess ||
         hipMalloc(&c.d_hist[0], hb) != hipSuccess || hipMalloc(&c.d_hist[1], hb) != hipSuccess ||
-        hipMemset(c.d_hist[0], 0, hb) != hipSuccess || hipMalloc(&c.d_best, 4) != hipSuccess) {
+        hipMemset(c.d_hist[0], 0, hb) != hipSuccess || hipMalloc(&c.d_best, 32) != hipSuccess) {
         set_error("corr_create: device allocation failed");
         srcdsp_corr_destroy(h);
         return SRCDSP_ERR_HIP;
