@@ -642,8 +642,9 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
             ew[idx - lo] = words[5 + (last - idx)];
         }
     } else {
-        SRCDSP_HIP_TRY(hipMemcpy(cw, c.d_corr + lo, 4 * cnt, hipMemcpyDeviceToHost));
-        SRCDSP_HIP_TRY(hipMemcpy(ew, c.d_en + lo, 4 * cnt, hipMemcpyDeviceToHost));
+        SRCDSP_HIP_TRY(hipMemcpyAsync(cw, c.d_corr + lo, 4 * cnt, hipMemcpyDeviceToHost, s));
+        SRCDSP_HIP_TRY(hipMemcpyAsync(ew, c.d_en + lo, 4 * cnt, hipMemcpyDeviceToHost, s));
+        SRCDSP_HIP_TRY(hipStreamSynchronize(s));
     }
     uint32_t nc[3], ne[3];
     for (int k = 0; k < 3; ++k) {  // nc[k] = corr of sample last-k
@@ -664,11 +665,12 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
         // effective stream positions best-NS .. best
         const long first = (long)best - (long)c.NS;
         std::vector<uint32_t> h_hist(NSm1 > 0 ? NSm1 : 1);
-        if (NSm1 > 0) SRCDSP_HIP_TRY(hipMemcpy(h_hist.data(), hist, 4 * NSm1, hipMemcpyDeviceToHost));
+        if (NSm1 > 0) SRCDSP_HIP_TRY(hipMemcpyAsync(h_hist.data(), hist, 4 * NSm1, hipMemcpyDeviceToHost, s));
         const long in_lo = std::max(0L, first);
         const long in_cnt = (long)best - in_lo + 1;
         std::vector<uint32_t> h_in(in_cnt);
-        SRCDSP_HIP_TRY(hipMemcpy(h_in.data(), d_in + in_lo, 4 * in_cnt, hipMemcpyDeviceToHost));
+        SRCDSP_HIP_TRY(hipMemcpyAsync(h_in.data(), d_in + in_lo, 4 * in_cnt, hipMemcpyDeviceToHost, s));
+        SRCDSP_HIP_TRY(hipStreamSynchronize(s));
         for (long j = first; j <= (long)best; ++j) {
             uint32_t v;
             if (j >= 0) v = h_in[j - in_lo];
@@ -829,8 +831,9 @@ SRCDSP_API int srcdsp_corr_reset(srcdsp_corr_t h) {
     for (int k = 0; k < 3; ++k) c.energy[k] = c.corr[k] = 0;
     std::fill(c.bits.begin(), c.bits.end(), 0);
     const size_t hb = 4 * (size_t)std::max(1u, c.NS - 1);
-    SRCDSP_HIP_TRY(hipMemset(c.d_hist[c.cur], 0, hb));
-    SRCDSP_HIP_TRY(hipDeviceSynchronize());
+    // on the handle's own stream: no wait on other streams' work
+    SRCDSP_HIP_TRY(hipMemsetAsync(c.d_hist[c.cur], 0, hb, c.stage.stream));
+    SRCDSP_HIP_TRY(hipStreamSynchronize(c.stage.stream));
     return SRCDSP_OK;
 }
 

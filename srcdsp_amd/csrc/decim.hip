@@ -424,8 +424,9 @@ int FirCore::clone_from(FirCore &src) {
 int FirCore::clear_history() {
     int rc = order.sync();
     if (rc) return rc;
-    for (int b = 0; b < 2; ++b) SRCDSP_HIP_TRY(hipMemset(d_hist[b], 0, hist_cap));
-    SRCDSP_HIP_TRY(hipDeviceSynchronize());
+    // on the handle's own stream: no wait on other streams' work
+    for (int b = 0; b < 2; ++b) SRCDSP_HIP_TRY(hipMemsetAsync(d_hist[b], 0, hist_cap, stage.stream));
+    SRCDSP_HIP_TRY(hipStreamSynchronize(stage.stream));
     return SRCDSP_OK;
 }
 

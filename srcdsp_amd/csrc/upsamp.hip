@@ -721,8 +721,9 @@ SRCDSP_API int srcdsp_up_reset(srcdsp_up_t h) {
     SRCDSP_ARG_CHECK(h != nullptr, "up_reset: null handle");
     int rc = h->u.order.sync();
     if (rc) return rc;
-    for (int b = 0; b < 2; ++b) SRCDSP_HIP_TRY(hipMemset(h->u.d_hist[b], 0, h->u.hist_cap));
-    SRCDSP_HIP_TRY(hipDeviceSynchronize());
+    // on the handle's own stream: no wait on other streams' work
+    for (int b = 0; b < 2; ++b) SRCDSP_HIP_TRY(hipMemsetAsync(h->u.d_hist[b], 0, h->u.hist_cap, h->u.stage.stream));
+    SRCDSP_HIP_TRY(hipStreamSynchronize(h->u.stage.stream));
     return SRCDSP_OK;
 }
 
