@@ -751,7 +751,9 @@ def main():
         scanned = (idx + 2) if found else L  # single-buffer reference scan length
         dot2_tops = 2048.0 * scanned / world / (kern_avg_ms * 1e-3) / 1e12  # per GPU
         roof = {"bound": "valu", "achieved": round(dot2_tops, 2), "peak": VALU_PEAK_TOPS,
-                "unit": "T v_dot2 lane-ops/s", "frac": round(dot2_tops / VALU_PEAK_TOPS, 4), "traffic": None,
+                "unit": "T v_dot2 lane-ops/s", "frac": round(dot2_tops / VALU_PEAK_TOPS, 4),
+                # HBM bytes per launch (PMC), as for the other VALU-bound lines
+                "traffic": traffic, "traffic_source": traffic_note,
                 "kernel": work.name, "kernel_ms": round(kern_avg_ms, 4), "scanned_samples": int(scanned),
                 "hbm_gbs_for_reference": round(achieved, 1)}
 
