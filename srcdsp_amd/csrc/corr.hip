@@ -296,7 +296,7 @@ __global__ __launch_bounds__(kCBlock) void corr_eval_dot2(const uint32_t *__rest
 }
 
 // ------------------------------------ S == 1: one launch, detection fused
-// corr_eval_dot2's arithmetic (S = 1, N % 16 = 0) over the whole call in ONE launch, with the
+// corr_eval_dot2's arithmetic at S = 1 (taps front-padded to NP) over the whole call in ONE launch, with the
 // peak/threshold test of correlators.h:262-268 evaluated by each block on its
 // own 4096 outputs and reduced to the first hit with atomicMin(best).
 //  * the test at a block's first two outputs needs corr/energy of the two
@@ -319,7 +319,7 @@ __device__ __forceinline__ unsigned load_best(const unsigned *best) {
 
 __global__ __launch_bounds__(kCBlock) void corr_scan_s1(const uint32_t *__restrict__ in, long n,
                                                          const uint32_t *__restrict__ hist,
-                                                         const uint32_t *__restrict__ ptaps, int N, unsigned cs,
+                                                         const uint32_t *__restrict__ ptaps, int N, int NP, unsigned cs,
                                                          uint32_t c_prev0, uint32_t c_prev1, uint32_t e_prev0,
                                                          uint32_t *__restrict__ corr_out,
                                                          uint32_t *__restrict__ en_out, unsigned *best) {
@@ -331,8 +331,10 @@ __global__ __launch_bounds__(kCBlock) void corr_scan_s1(const uint32_t *__restri
     if (threadIdx.x == 0) best0 = load_best(best);
     __syncthreads();
     if ((long)best0 < i0) return;  // a hit before this tile is already known (block-uniform)
-    const long base = i0 - (N - 1);
-    const int span = TO + N - 1;
+    // taps front-padded with NP - N zero taps (NP = 16 ceil(N/16), as corr_eval_dot2)
+    const long base = i0 - (NP - 1);
+    const int span = TO + NP - 1;
+    const int pad = NP - N;
     auto lw = [&](int l) { int lp = l + 1; return lp + 4 * (lp / kCR); };
     for (int l = threadIdx.x; l < span; l += kCBlock) {
         long j = base + l;
@@ -382,7 +384,7 @@ __global__ __launch_bounds__(kCBlock) void corr_scan_s1(const uint32_t *__restri
     };
     bool dead = false;
     int m0 = 0;
-    for (int it = 0; m0 + 32 <= N; m0 += 32, ++it) {
+    for (int it = 0; m0 + 32 <= NP; m0 += 32, ++it) {
         chunk(m0, A, B);
         chunk(m0 + 16, B, A);
         if ((it & 7) == 7) {  // every 256 taps: has a hit before this tile been found?
@@ -393,7 +395,7 @@ __global__ __launch_bounds__(kCBlock) void corr_scan_s1(const uint32_t *__restri
             }
         }
     }
-    if (!dead && m0 < N) chunk(m0, A, B);
+    if (!dead && m0 < NP) chunk(m0, A, B);
     // the two outputs before the tile (for the test at its first two indices)
     if (t < 64) {
         uint32_t ex_c[2] = {c_prev0, c_prev1}, ex_e = e_prev0;
@@ -403,8 +405,8 @@ __global__ __launch_bounds__(kCBlock) void corr_scan_s1(const uint32_t *__restri
                 const uint32_t xa = corr_fetch(in, hist, i0 - N + m, N - 1);      // u = 0
                 const uint32_t xb = corr_fetch(in, hist, i0 - N - 1 + m, N - 1);  // u = 1
                 const short2_t sa = __builtin_bit_cast(short2_t, xa), sb = __builtin_bit_cast(short2_t, xb);
-                const short2_t p0 = __builtin_bit_cast(short2_t, (uint32_t)tp[2 * m]);
-                const short2_t p1 = __builtin_bit_cast(short2_t, (uint32_t)tp[2 * m + 1]);
+                const short2_t p0 = __builtin_bit_cast(short2_t, (uint32_t)tp[2 * (m + pad)]);
+                const short2_t p1 = __builtin_bit_cast(short2_t, (uint32_t)tp[2 * (m + pad) + 1]);
                 r1 = __builtin_amdgcn_sdot2(sa, p0, r1, false);
                 q1 = __builtin_amdgcn_sdot2(sa, p1, q1, false);
                 r2 = __builtin_amdgcn_sdot2(sb, p0, r2, false);
@@ -431,11 +433,15 @@ __global__ __launch_bounds__(kCBlock) void corr_scan_s1(const uint32_t *__restri
     }
     // this lane's correlation values and (sliding) energies
     uint32_t cv[kCR], ev[kCR];
-    uint32_t e = (uint32_t)e0;
+    uint32_t e = (uint32_t)e0;  // the direct sum ran over NP window words, the first pad before the real window
+    for (int q = 0; q < pad; ++q) {
+        const short2_t a = __builtin_bit_cast(short2_t, xs[lw(lb + q)]);
+        e -= (uint32_t)__builtin_amdgcn_sdot2(a, a, 0, false);
+    }
 #pragma unroll
     for (int r = 0; r < kCR; ++r) {
         if (r > 0) {  // E_i = E_{i-1} + |x_i|^2 - |x_{i-N}|^2
-            const uint32_t xn = xs[lw(lb + r + N - 1)], xo = xs[lw(lb + r - 1)];
+            const uint32_t xn = xs[lw(lb + r + NP - 1)], xo = xs[lw(lb + r - 1 + pad)];
             const short2_t a = __builtin_bit_cast(short2_t, xn), b = __builtin_bit_cast(short2_t, xo);
             e += (uint32_t)__builtin_amdgcn_sdot2(a, a, 0, false) - (uint32_t)__builtin_amdgcn_sdot2(b, b, 0, false);
         }
@@ -564,11 +570,11 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
     const unsigned cs = (unsigned)c.coeff_scaling;
     // dot2 tiles for int16-range patterns (48 <= N <= kCorrDot2MaxTaps, any
     // S: below 48 taps the one-output-per-lane kernel is faster, 0.277 vs
-    // 0.468 ms at N = 31, S = 3 on 2^24 samples); S = 1 with N % 16 = 0
-    // (config 5) scans in one launch with detection fused
+    // 0.468 ms at N = 31, S = 3 on 2^24 samples); at S = 1 (config 5 and
+    // any other N they take) one launch scans with detection fused
     const bool dot2 = c.taps16 && c.NP <= kCorrDot2MaxTaps && c.S <= kCorrMaxGridY &&
                       (c.N >= 48 || (c.S == 1 && c.N % 16 == 0));
-    const bool fast = dot2 && c.S == 1 && c.N % 16 == 0;
+    const bool fast = dot2 && c.S == 1;
     // the fused scan keeps no per-sample values (corr_point computes the three
     // the registers need); the segmented kernels write corr/energy per sample
     // for corr_detect
@@ -588,9 +594,9 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
     if (fused) {  // one launch, detection fused, in-flight early exit
         constexpr long TO = (long)kCBlock * kCR;
         const long blocks = (n + TO - 1) / TO;
-        const size_t smem = 4 * (size_t)(((TO + c.N + 1) / kCR + 2) * (kCR + 4));
+        const size_t smem = 4 * (size_t)(((TO + c.NP + 1) / kCR + 2) * (kCR + 4));
         hipLaunchKernelGGL(corr_scan_s1, dim3((unsigned)blocks), dim3(kCBlock), smem, s, d_in, n, hist, c.d_ptaps,
-                           (int)c.N, cs, c.corr[0], c.corr[1], c.energy[0], nullptr, nullptr, c.d_best);
+                           (int)c.N, (int)c.NP, cs, c.corr[0], c.corr[1], c.energy[0], nullptr, nullptr, c.d_best);
         SRCDSP_HIP_TRY(hipGetLastError());
         hipLaunchKernelGGL(corr_point, dim3(1), dim3(256), 0, s, d_in, n, hist, c.d_coef, c.N, c.S, cs,
                            (const unsigned *)c.d_best, c.d_best + 2);
