@@ -1,6 +1,6 @@
 """Kernel time of the FixedPatternCorrelator step across (N, S): the fused
-one-launch scan (S = 1, N % 16 = 0: config 5's shape), the dot2 tiles for any
-other N and stride, and (past 8192 taps) the generic kernel.
+one-launch scan (S = 1, any N >= 48 or N % 16 = 0: config 5's shape among them),
+the dot2 tiles for any other N and stride, and (past 8192 taps) the generic kernel.
 
   python scripts/corr_envelope.py [N:S ...]
 
