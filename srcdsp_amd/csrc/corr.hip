@@ -568,12 +568,12 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
     const long NSm1 = (long)c.NS - 1;
     const uint32_t *hist = c.d_hist[c.cur];
     const unsigned cs = (unsigned)c.coeff_scaling;
-    // dot2 tiles for int16-range patterns (48 <= N <= kCorrDot2MaxTaps, any
-    // S: below 48 taps the one-output-per-lane kernel is faster, 0.277 vs
-    // 0.468 ms at N = 31, S = 3 on 2^24 samples); at S = 1 (config 5 and
-    // any other N they take) one launch scans with detection fused
+    // dot2 tiles for int16-range patterns (48 <= N <= kCorrDot2MaxTaps at
+    // S > 1: below 48 taps there the strided staging costs more than the taps,
+    // 0.277 vs 0.468 ms at N = 31, S = 3 on 2^24 samples); at S = 1 (config 5
+    // and every N <= kCorrDot2MaxTaps) one launch scans with detection fused
     const bool dot2 = c.taps16 && c.NP <= kCorrDot2MaxTaps && c.S <= kCorrMaxGridY &&
-                      (c.N >= 48 || (c.S == 1 && c.N % 16 == 0));
+                      (c.N >= 48 || c.S == 1);
     const bool fast = dot2 && c.S == 1;
     // the fused scan keeps no per-sample values (corr_point computes the three
     // the registers need); the segmented kernels write corr/energy per sample
