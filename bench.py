@@ -5,10 +5,12 @@ Default workload = BASELINE.json configs[1] (the headline metric): the 127-tap
 complex<float> decimate-by-4 FilterDnsamplingFir over 2^28 device-resident
 synthetic samples, one step() per timed step (one kernel launch), FMA float
 contract.  With --gpus N (launched by torch.distributed.run) every rank owns
-the same work as N = 1 (one 2^28-sample channel; --channels-per-gpu 8 at N = 8
-gives configs[2]'s 64 channels over 8 GPUs, one batched launch per step per
-rank): weak scaling, no collective in the timed region; the RCCL result gather
-to rank 0 is timed separately (gather_ms).
+8 channels of 2^28 samples (configs[2]'s layout: 64 channels over 8 GPUs at
+N = 8, one batched launch per step per rank; --channels-per-gpu overrides):
+weak scaling, no collective in the timed region; the RCCL gather of every
+channel's decimated output to rank 0 (32 GiB at N = 8) is timed separately
+(gather_ms).  N = 1 stays configs[1] (one channel), so SCALE's N = 1 value is
+BENCH's.
 
 Other workloads (--workload): mixdecim (config 4, mixer -> fixed-point
 decimator, fused), corr (config 5, 1024-lag correlator), fir (config 1 shape on
@@ -51,9 +53,9 @@ def parse():
     p.add_argument("--workload", default="decim", choices=["decim", "mixdecim", "ci16decim", "corr", "fir", "up", "fifo", "iq"])
     p.add_argument("--samples", type=int, default=None,
                    help="input samples per channel per step (default 2^28; corr: 2^26, config 5's 64 Msamp)")
-    # default 1 channel per GPU at every N (configs[1]'s work on each rank, so
-    # per-GPU work is fixed as N grows); 8 at N = 8 is configs[2]'s 64 channels
-    p.add_argument("--channels-per-gpu", type=int, default=1)
+    # default (decim): 1 channel at N = 1 (configs[1]), 8 per GPU at N > 1
+    # (configs[2]: 64 channels at N = 8); see channel_layout()
+    p.add_argument("--channels-per-gpu", type=int, default=None)
     p.add_argument("--fp", default="fma", choices=["fma", "strict"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=1 << 27, help="samples timed on the reference CPU path")
@@ -91,6 +93,27 @@ def spawn_ranks(args) -> int | None:
     return subprocess.run(cmd).returncode
 
 
+def channel_layout(args, world: int, L: int | None = None) -> dict:
+    """Channel layout of the decim workload (BASELINE configs[1] / configs[2]).
+    N = 1: one 2^28-sample channel (configs[1], the headline).  N > 1: 8
+    channels per GPU, block-partitioned (srcdsp_amd.dist.channels_for_rank),
+    so N = 8 holds configs[2]'s 64 independent 256 Msamp channels; the gather
+    moves every channel's decimated output (L/4 complex<float>) to rank 0.
+    Other workloads run one buffer per rank."""
+    if L is None:
+        L = args.samples if args.samples is not None else (1 << 28)
+        L -= L % 4
+    if args.workload != "decim":
+        cpg = 1
+    elif args.channels_per_gpu is not None:
+        cpg = args.channels_per_gpu
+    else:
+        cpg = 1 if world == 1 else 8
+    total = cpg * world
+    return {"channels_per_gpu": cpg, "channels_total": total, "samples_per_channel": L,
+            "gather_bytes": total * (L // 4) * 8 if args.workload == "decim" and world > 1 else 0}
+
+
 def dry_run(args) -> None:
     """One line per rank: the rank/world the launcher gave it and the world a
     gloo process group actually assembled (an all-reduce of ones).  No GPU."""
@@ -109,7 +132,8 @@ def dry_run(args) -> None:
     # print() (text, then newline) from two ranks can interleave on one line
     sys.stdout.flush()
     os.write(1, (json.dumps({"dry_run": True, "rank": rank, "world": world, "world_seen": seen,
-                             "gpus": args.gpus}) + "\n").encode())
+                             "gpus": args.gpus, "workload": args.workload,
+                             "layout": channel_layout(args, world)}) + "\n").encode())
     if world != args.gpus or seen != args.gpus:
         raise SystemExit(f"bench: rank {rank} sees world {world}/{seen}, --gpus {args.gpus}")
 
@@ -656,8 +680,8 @@ def main():
     if args.samples is None:
         args.samples = (1 << 26) if args.workload == "corr" else (1 << 28)
     L = args.samples - args.samples % 4
-    if args.workload != "decim":
-        args.channels_per_gpu = 1
+    lay = channel_layout(args, world, L)
+    args.channels_per_gpu = lay["channels_per_gpu"]
     work = WORKLOADS[args.workload](S, torch, L, args.channels_per_gpu, rank, args.fp)
     stream = torch.cuda.current_stream()
 
@@ -759,6 +783,10 @@ def main():
 
     if rank == 0:
         cfg = {"workload": work.name, "samples_per_channel": L, "channels_per_gpu": args.channels_per_gpu,
+               "channels_total": lay["channels_total"],
+               "baseline_config": ("configs[1]" if world == 1 and lay["channels_total"] == 1 else
+                                   "configs[2]" if lay["channels_per_gpu"] == 8 else "custom")
+               if args.workload == "decim" else None,
                "taps": {"decim": 127, "mixdecim": 127, "ci16decim": 127, "fir": 31, "up": 128}.get(args.workload),
                "decimation": {"decim": 4, "mixdecim": 4, "ci16decim": 4}.get(args.workload), "interpolation": 4 if args.workload == "up" else None,
                "fp_contract": args.fp,
@@ -777,9 +805,19 @@ def main():
                 "data": "synthetic (counter-based splitmix64 integer samples, SURVEY §8d)", "config": cfg,
                 "roofline": roof, "hbm_read": hbm_read, "world_size_reported": reported,
                 "backend": BACKEND if world > 1 else None}
+        if args.workload == "decim":
+            # `roofline` is rank 0's own batched launch (its channels_per_gpu
+            # channels), i.e. per GPU; at N > 1 one launch covers 8 channels and
+            # the clock holds steady across it, whereas the N = 1 line times one
+            # 2^28 channel per launch inside the post-idle clock transient
+            # (DESIGN §5.1), so the per-GPU fraction differs between the two
+            roof["per_gpu"] = True
+            roof["channels_per_launch"] = args.channels_per_gpu
         if gather_ms is not None:
             line["gather_ms"] = round(gather_ms, 3)
             line["gather_bytes"] = int(world * work.y.numel() * work.y.element_size())
+            assert line["gather_bytes"] == lay["gather_bytes"]
+            line["gather_gbs"] = round(line["gather_bytes"] / (gather_ms * 1e-3) / 1e9, 1)
         if args.workload == "corr":
             line["detection"] = list(work.last)
         if not args.no_cpu_baseline and world == 1:

@@ -40,10 +40,12 @@ public:
     }
     /// mixers.h:169-188 (non-const input, as the reference)
     void step(std::vector<std::complex<int16_t>> &in, std::vector<std::complex<int16_t>> &out) {
+        srcdsp_detail::check_size(out.size() >= in.size(), "Mixer::step");
         srcdsp_detail::check(srcdsp_mixer_step_host(h_, in.data(), in.size(), out.data()), "Mixer::step");
     }
     void step(const DeviceSpan<const std::complex<int16_t>> &in, DeviceSpan<std::complex<int16_t>> out,
               void *stream = nullptr) {
+        srcdsp_detail::check_size(out.size >= in.size, "Mixer::step(device)");
         srcdsp_detail::check(srcdsp_mixer_step(h_, in.data, in.size, out.data, stream), "Mixer::step(device)");
     }
     srcdsp_mixer_t handle() const { return h_; }

@@ -44,6 +44,14 @@ inline void check(int rc, const char *what) {
     }
 }
 
+/// An output buffer shorter than the call writes: the reference writes past
+/// its end (undefined behaviour, e.g. mixers.h:172-175); here it asserts, and
+/// with NDEBUG throws std::length_error before any byte is staged or launched.
+inline void check_size(bool ok, const char *what) {
+    assert(ok && "output buffer smaller than the call writes");
+    if (!ok) throw std::length_error(std::string(what) + ": output buffer smaller than the input");
+}
+
 template <class T> struct kind;  // sample / coefficient type codes
 template <> struct kind<std::complex<float>> { static constexpr int v = 0; };
 template <> struct kind<std::complex<int16_t>> { static constexpr int v = 1; };

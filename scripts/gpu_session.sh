@@ -11,6 +11,10 @@
 #   prof             rocprofv3 --kernel-trace --stats of bench.py ${BENCH_ARGS} (per-dispatch CSV kept)
 #   pmc              FETCH_SIZE / WRITE_SIZE passes (scripts/pmc_traffic.py) for each of ${PMC_WORKLOADS}
 #   ramp             cold ramps of tune variants ${VARIANTS} (scripts/tune/ramp.py), IDLE s apart
+#   wpower           socket power / clock / limiter counters through a cold start (scripts/tune/window_power.py)
+#                    for each tap count of ${WP_TAPS} (default 127)
+#   phase            per-phase cycles of the config-4 kernel (scripts/tune/phase_clock.py; tuning build
+#                    scripts/tune/ab/libsrcdsp_hip_phase.so)
 #   envelope         scripts/shape_envelope.py ${ENV_M}
 #   census           workgroup placement census (scripts/tune/census.py)
 #   ab               same-box A/B of scripts/tune/ab/libsrcdsp_hip_base.so vs the tree's library
@@ -54,6 +58,12 @@ for s in ${STEPS:-smoke tests bench}; do
         step ramp_${TAG}_$v 150 python3 -u scripts/tune/ramp.py $v ${LAUNCHES:-300}
         tail -n 1 gpurun_out/ramp_${TAG}_$v.log >> gpurun_out/ramp_$TAG.jsonl
       done ;;
+    wpower)
+      for tp in ${WP_TAPS:-127}; do
+        step wpower_${TAG}_$tp 120 python3 -u scripts/tune/window_power.py ${LAUNCHES:-300} ${IDLE:-8} $tp
+      done ;;
+    phase) SRCDSP_HIP_LIB=$PWD/scripts/tune/ab/libsrcdsp_hip_phase.so \
+             step phase_$TAG 120 python3 -u scripts/tune/phase_clock.py ${PHASE_WL:-mixdecim} ;;
     envelope) step envelope_$TAG 600 python -u scripts/shape_envelope.py ${ENV_M} ;;
     census) step census_$TAG 120 python -u scripts/tune/census.py ;;
     ab) step ab_$TAG 1000 bash scripts/tune/ab_libs.sh ;;

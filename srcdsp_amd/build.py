@@ -93,17 +93,22 @@ def _stale(target: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(verbose: bool = False, jobs: int = 8) -> str:
+def build(verbose: bool = False, jobs: int = 8, defines: tuple[str, ...] = (), lib: str | None = None) -> str:
+    """Compile and link the library.  `defines`/`lib`: a tuning build (e.g.
+    ("SRCDSP_TUNING", "SRCDSP_PHASE_CLOCK") into scripts/tune/ab/...), with its
+    own object directory; the product build takes neither."""
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
-    os.makedirs(OBJ, exist_ok=True)
-    os.makedirs(LIB_DIR, exist_ok=True)
+    obj_dir = OBJ if not defines else OBJ + "_" + "_".join(d.lower() for d in defines)
+    LIB = lib or globals()["LIB"]
+    os.makedirs(obj_dir, exist_ok=True)
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
     hipcc = _hipcc()
     hdrs = _headers()
 
     def compile_one(src: str) -> str:
-        obj = os.path.join(OBJ, os.path.basename(src) + ".o")
+        obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
         if _stale(obj, [src] + hdrs):
-            cmd = [hipcc, *CXXFLAGS, "-c", src, "-o", obj]
+            cmd = [hipcc, *CXXFLAGS, *[f"-D{d}" for d in defines], "-c", src, "-o", obj]
             if verbose:
                 print(" ".join(cmd), file=sys.stderr)
             r = subprocess.run(cmd, capture_output=True, text=True)
@@ -127,4 +132,10 @@ def build(verbose: bool = False, jobs: int = 8) -> str:
 
 
 if __name__ == "__main__":
-    print(build(verbose=True))
+    # python -m srcdsp_amd.build [NAME DEFINE...]: with arguments, a tuning
+    # build scripts/tune/ab/libsrcdsp_hip_NAME.so compiled with -DDEFINE...
+    if len(sys.argv) > 2:
+        print(build(verbose=True, defines=tuple(sys.argv[2:]),
+                    lib=os.path.join(ROOT, "scripts", "tune", "ab", f"libsrcdsp_hip_{sys.argv[1]}.so")))
+    else:
+        print(build(verbose=True))

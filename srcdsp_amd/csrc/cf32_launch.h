@@ -28,15 +28,20 @@ template <int M>
 constexpr int cf32_r() { return M == 1 ? 8 : (M <= 3 ? 4 : 16 / M); }
 
 // allow a kernel's dynamic LDS beyond the default limit (once per kernel and size)
-inline void raise_lds_limit(const void *kern, size_t bytes) {
+inline int raise_lds_limit(const void *kern, size_t bytes) {
     static std::mutex mu;
     static std::map<const void *, size_t> set;
     std::lock_guard<std::mutex> g(mu);
     size_t &cur = set[kern];
     if (bytes > cur) {
-        (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        hipError_t e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        if (e != hipSuccess) {  // not cached: the next call tries again
+            set_error(std::string("hipFuncSetAttribute(MaxDynamicSharedMemorySize): ") + hipGetErrorString(e));
+            return SRCDSP_ERR_HIP;
+        }
         cur = bytes;
     }
+    return SRCDSP_OK;
 }
 
 template <int NT, int M = 4>
@@ -54,19 +59,21 @@ int launch_cf32(DecimLaunch L, int channels, bool fma, hipStream_t s) {
     // taps issued tap-major through inline asm (FMA: 0.88 M instead of
     // 1.08 M cycles per launch, -8.6 % time on one box,
     // profiles/tuning/r02_ramp_ab.txt)
-    auto go = [&](auto kern) {
-        if (NT == 0) raise_lds_limit((const void *)kern, smem);
+    auto go = [&](auto kern) -> int {
+        if (NT == 0) {
+            int rc = raise_lds_limit((const void *)kern, smem);
+            if (rc) return rc;
+        }
         hipLaunchKernelGGL(kern, grid, dim3(kCfBlock), smem, s, L);
+        return SRCDSP_OK;
     };
     if (fma && q0)
-        go(decim_stream_cf32<NT, R, kCfBlock, true, 4, true, M>);
-    else if (fma)
-        go(decim_stream_cf32<NT, R, kCfBlock, true, 4, false, M>);
-    else if (q0)
-        go(decim_stream_cf32<NT, R, kCfBlock, false, 4, true, M>);
-    else
-        go(decim_stream_cf32<NT, R, kCfBlock, false, 4, false, M>);
-    return SRCDSP_OK;
+        return go(decim_stream_cf32<NT, R, kCfBlock, true, 4, true, M>);
+    if (fma)
+        return go(decim_stream_cf32<NT, R, kCfBlock, true, 4, false, M>);
+    if (q0)
+        return go(decim_stream_cf32<NT, R, kCfBlock, false, 4, true, M>);
+    return go(decim_stream_cf32<NT, R, kCfBlock, false, 4, false, M>);
 }
 
 }  // namespace srcdsp

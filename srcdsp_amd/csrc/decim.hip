@@ -84,6 +84,17 @@ static int ci16_variant() {
 }
 #endif
 
+#ifdef SRCDSP_PHASE_CLOCK
+// tuning build: read (and clear) decim_dot2_ci16's phase clock sums
+extern "C" SRCDSP_API int srcdsp_tune_phase_clock(unsigned long long *out8) {
+    SRCDSP_HIP_TRY(hipDeviceSynchronize());
+    SRCDSP_HIP_TRY(hipMemcpyFromSymbol(out8, HIP_SYMBOL(phase_clock), 8 * sizeof(unsigned long long)));
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    SRCDSP_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(phase_clock), z, sizeof z));
+    return SRCDSP_OK;
+}
+#endif
+
 // period of the fused mixer's table index over input samples, extended to a
 // multiple of 4 (one 16-B table read per staged granule): lcm(N / gcd(freq, N), 4)
 static unsigned mixer_seq_period(unsigned N, unsigned fr) {
@@ -727,8 +738,10 @@ SRCDSP_API int srcdsp_fir_step_host(srcdsp_fir_t h, const void *in, size_t n_in,
 // -------------------------------------------------- Mixer -> decimator chain
 // The two reference calls as two launches, through the mixer handle's
 // grow-only scratch buffer: the configurations the fused kernel does not
-// cover.  The scratch is rewritten only after the decimator's previous step
-// (its last reader) on this stream.
+// cover.  The mixer's ordering event is recorded after the DECIMATOR launch
+// (the scratch's reader), so the next mixer write into the scratch -- from
+// whichever decimator and stream the mixer feeds next -- waits for the last
+// read of it, not only for the last mixer kernel.
 static int mixdecim_unfused(srcdsp_mixer_t mixer, FirCore &f, const void *d_in, size_t n_in, void *d_out,
                             size_t n_out, hipStream_t s) {
     MixerState &m = mixer->m;
@@ -747,6 +760,7 @@ static int mixdecim_unfused(srcdsp_mixer_t mixer, FirCore &f, const void *d_in, 
     if (rc) return rc;
     rc = srcdsp_mixer_step(mixer, d_in, n_in, m.d_scratch, s);  // mixers.h:169-188
     if (rc == SRCDSP_OK) rc = core_step(f, m.d_scratch, n_in, d_out, n_out, s, nullptr);
+    if (rc == SRCDSP_OK) rc = m.order.after(s);  // scratch released after its reader
     return rc;
 }
 

@@ -468,6 +468,25 @@ namespace srcdsp {
 // next tile's prefetch) and output stores stay in flight across the barrier.
 #define SRCDSP_LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 
+// Phase clock of decim_dot2_ci16 (tuning builds only, -DSRCDSP_PHASE_CLOCK,
+// scripts/tune/phase_clock.py): every wave sums the shader cycles (s_memtime)
+// it spends in each phase of its tile loop, and lane 0 adds the sums to
+// phase_clock[] (vector atomics) at exit:
+//   0 prologue (table build, history, first staging load), 1 wait at the
+//   barrier before staging, 2 staging (mix + LDS writes), 3 wait at the
+//   barrier after staging (+ next tile's load issue), 4 tap loop + quantise,
+//   5 stores, 6 waves, 7 tiles.
+// The stamps wait for outstanding LDS reads (lgkmcnt), so they perturb the
+// schedule a little; they are a diagnosis, not a timing.
+#ifdef SRCDSP_PHASE_CLOCK
+static __device__ unsigned long long phase_clock[8];
+#define SRCDSP_PH(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define SRCDSP_PH_ADD(k, d) ph_acc[k] += (d)
+#else
+#define SRCDSP_PH(v)
+#define SRCDSP_PH_ADD(k, d)
+#endif
+
 
 }  // namespace srcdsp
 namespace srcdsp {
@@ -1389,6 +1408,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     const int TG = (SPT + HS) / 4;                // staged 16-B sample granules
     __shared__ uint4 lds[LSLOTS];
     __shared__ __attribute__((aligned(16))) uint32_t ctab[TABMAX];
+#ifdef SRCDSP_PHASE_CLOCK
+    unsigned long long ph_acc[8] = {0, 0, 0, 0, 0, 0, 1, 0};
+#endif
+    SRCDSP_PH(ph_start);
 
     const int ch = blockIdx.y;
     const uint32_t *in = (const uint32_t *)a.in + ch * a.in_stride;
@@ -1553,8 +1576,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
             stage_load(t_begin);
         }
     }
+    SRCDSP_PH(ph_loop);
+    SRCDSP_PH_ADD(0, ph_loop - ph_start);
     for (long tile = t_begin; tile < t_end; ++tile) {
+        SRCDSP_PH(ph0);
         SRCDSP_LDS_BARRIER();
+        SRCDSP_PH(ph1);
         if (MIX && SEQT && tile != 0) {
             unsigned m = m_tile;  // wave-uniform
 #pragma unroll
@@ -1586,9 +1613,11 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
                 if (g < TG) put(g, v[i].x, v[i].y, v[i].z, v[i].w);
             }
         }
+        SRCDSP_PH(ph2);
         SRCDSP_LDS_BARRIER();
         if constexpr (MIX && SEQT) m_tile = advp(m_tile, a.mix_pe_dtile);
         if (tile + 1 < t_end) stage_load(tile + 1);
+        SRCDSP_PH(ph3);
 
         ConstPtr<uint32_t> tp = const_view<uint32_t>(a.coef);
         asm volatile("" : "+s"(tp));
@@ -1745,6 +1774,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
             pass(std::integral_constant<int, 0>{});
             if constexpr (RSTEP == 2) pass(std::integral_constant<int, 1>{});
         }
+        SRCDSP_PH(ph4);
         const long n0 = tile * TO + (long)t * R;
         if (n0 + R <= a.n_out) {
             if constexpr (R >= 4) {
@@ -1760,13 +1790,26 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
             for (int r = 0; r < R; ++r)
                 if (n0 + r < a.n_out) out[n0 + r] = w[r];
         }
+        SRCDSP_PH(ph5);
+        SRCDSP_PH_ADD(1, ph1 - ph0);
+        SRCDSP_PH_ADD(2, ph2 - ph1);
+        SRCDSP_PH_ADD(3, ph3 - ph2);
+        SRCDSP_PH_ADD(4, ph4 - ph3);
+        SRCDSP_PH_ADD(5, ph5 - ph4);
+        SRCDSP_PH_ADD(7, 1);
     }
+#ifdef SRCDSP_PHASE_CLOCK
+    if ((t & 63) == 0)
+        for (int k = 0; k < 8; ++k) atomicAdd(&phase_clock[k], ph_acc[k]);
+#endif
 }
 
 // ------------------------------------------------------ single-rate float FIR
-// FilterFir (filters.h:133-169) and M = 1 decimators for complex<float> input
-// (KV_CF32) and float input -> complex<float> output with a zero imaginary
-// part (KV_F32_REAL), any tap count up to kFirMaxTaps (runtime).
+// FilterFir (filters.h:133-169) for float input -> complex<float> output
+// with a zero imaginary part (KV_F32_REAL), any tap count up to kFirMaxTaps
+// (runtime).  complex<float> FilterFir / M = 1 decimators run on the headline
+// kernel (decim_stream_cf32<0, R, ..., 1>, any N <= kCfMaxTaps), which takes
+// every complex<float> shape this kernel could.
 // Each lane owns R = 8 consecutive outputs; taps are walked in chunks of 4
 // with a 12-sample register window held as three 4-sample blocks A|B|C (tap
 // chunk q of output r reads sample r - 4q - p, p < 4).  After a chunk C drops,
@@ -1786,11 +1829,6 @@ template <>
 struct FirTraits<KV_F32_REAL> {
     typedef float S;
     static constexpr int SPG = 4;  // samples per 16-B granule
-};
-template <>
-struct FirTraits<KV_CF32> {
-    typedef float2 S;
-    static constexpr int SPG = 2;
 };
 
 __device__ __forceinline__ float fir_mac(bool fma, float c, float x, float y) {

@@ -17,6 +17,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -110,6 +112,11 @@ void comm_release(srcdsp_comm *c) {
     delete c;
 }
 
+bool shared_devices_allowed() {
+    const char *v = std::getenv("SRCDSP_COMM_SHARED_DEVICES");
+    return v && std::strcmp(v, "1") == 0;
+}
+
 // restores the caller's current device on scope exit
 struct DeviceGuard {
     int saved = -1;
@@ -131,7 +138,11 @@ SRCDSP_API int srcdsp_comm_create(srcdsp_comm_t *out, int ndev, const int *devs)
     for (int r = 0; r < ndev; ++r) {
         d[r] = devs ? devs[r] : r;
         SRCDSP_ARG_CHECK(d[r] >= 0 && d[r] < have, "comm_create: device id out of range");
-        for (int q = 0; q < r; ++q) SRCDSP_ARG_CHECK(d[q] != d[r], "comm_create: a device listed twice");
+        // RCCL refuses a communicator whose ranks share a device; a rehearsal
+        // of the multi-device logic on one GPU (a communicator library that
+        // allows it, tests/rccl_stub) opts in with SRCDSP_COMM_SHARED_DEVICES=1
+        if (!shared_devices_allowed())
+            for (int q = 0; q < r; ++q) SRCDSP_ARG_CHECK(d[q] != d[r], "comm_create: a device listed twice");
     }
     const Rccl &R = rccl();
     if (!R.ok) {

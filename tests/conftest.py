@@ -33,3 +33,10 @@ def S():
     import srcdsp_amd
     srcdsp_amd.lib()
     return srcdsp_amd
+
+
+@pytest.fixture(scope="session")
+def O():
+    """The oracle (test infrastructure): strict and FMA float contracts."""
+    import pyoracle
+    return {"strict": pyoracle.Oracle(0), "fma": pyoracle.Oracle(1)}

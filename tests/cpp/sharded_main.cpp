@@ -9,12 +9,14 @@
 //         tag 10+ch = channel ch's input (complex<float>), all the same length.
 // out.bin: tag 100+ch = channel ch by the host-vector step() in two chained
 //          calls; tag 200 = all channels by the device step() after reset(),
-//          gathered to the first device (channel-major).
+//          gathered to rank ROOT's device (channel-major; ROOT from the
+//          environment variable SHARDED_ROOT, default 0).
 #include <hip/hip_runtime.h>
 
 #include <complex>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <fstream>
 #include <map>
 #include <vector>
@@ -68,6 +70,11 @@ int main(int argc, char **argv) {
     std::vector<std::vector<cf32>> in(C);
     for (int ch = 0; ch < C; ++ch) in[ch] = as<cf32>(rec[10 + ch]);
     const size_t n = in[0].size(), n_out = n / 4, half = (n / 2) & ~(size_t)3;
+    const int root = std::getenv("SHARDED_ROOT") ? std::atoi(std::getenv("SHARDED_ROOT")) : 0;
+    if (root < 0 || root >= (int)devs.size()) {
+        std::fprintf(stderr, "SHARDED_ROOT out of range\n");
+        return 2;
+    }
     std::ofstream out(argv[2], std::ios::binary);
 
     dsptl::GpuComm comm(devs);
@@ -106,13 +113,13 @@ int main(int argc, char **argv) {
             HIP_OK(hipMemcpy(x + k * n, in[first + k].data(), n * sizeof(cf32), hipMemcpyHostToDevice));
         d_in[r] = x;
         d_out[r] = y;
-        if (r == 0) HIP_OK(hipMalloc(&d_root, (size_t)C * n_out * sizeof(cf32)));
+        if (r == root) HIP_OK(hipMalloc(&d_root, (size_t)C * n_out * sizeof(cf32)));
     }
     f.step(d_in, n, d_out, n_out, n);
-    f.gather(d_out, n_out, n_out, d_root, 0);
+    f.gather(d_out, n_out, n_out, d_root, root);
     comm.synchronize();
     std::vector<cf32> all((size_t)C * n_out);
-    HIP_OK(hipSetDevice(devs[0]));
+    HIP_OK(hipSetDevice(devs[root]));
     HIP_OK(hipMemcpy(all.data(), d_root, all.size() * sizeof(cf32), hipMemcpyDeviceToHost));
     put(out, 200, all.data(), (int64_t)(all.size() * sizeof(cf32)));
 
@@ -127,11 +134,14 @@ int main(int argc, char **argv) {
         HIP_OK(hipMalloc(&d_out2[r], std::max<size_t>(1, count * ostr) * sizeof(cf32)));
     }
     f.step(d_in, n, d_out2, ostr, n);
-    HIP_OK(hipSetDevice(devs[0]));
-    HIP_OK(hipMemset(d_root, 0, (size_t)C * n_out * sizeof(cf32)));
-    f.gather(d_out2, ostr, n_out, d_root, 0);
+    HIP_OK(hipSetDevice(devs[root]));
+    // on the root's comm stream: the gather's copies into d_root are ordered
+    // after it there (a plain hipMemset on the null stream is not ordered
+    // with the comm streams, which are non-blocking)
+    HIP_OK(hipMemsetAsync(d_root, 0, (size_t)C * n_out * sizeof(cf32), (hipStream_t)comm.stream(root)));
+    f.gather(d_out2, ostr, n_out, d_root, root);
     comm.synchronize();
-    HIP_OK(hipSetDevice(devs[0]));
+    HIP_OK(hipSetDevice(devs[root]));
     HIP_OK(hipMemcpy(all.data(), d_root, all.size() * sizeof(cf32), hipMemcpyDeviceToHost));
     put(out, 201, all.data(), (int64_t)(all.size() * sizeof(cf32)));
     for (int r = 0; r < R; ++r) {
@@ -146,8 +156,8 @@ int main(int argc, char **argv) {
         auto *g2 = new dsptl::ShardedDnsamplingFir<cf32, cf32, cf32, float, 4>(*c2, C, taps);
         delete c2;
         g2->step(d_in, n, d_out, n_out, n);
-        g2->gather(d_out, n_out, n_out, d_root, 0);
-        HIP_OK(hipSetDevice(devs[0]));
+        g2->gather(d_out, n_out, n_out, d_root, root);
+        HIP_OK(hipSetDevice(devs[root]));
         HIP_OK(hipDeviceSynchronize());
         HIP_OK(hipMemcpy(all.data(), d_root, all.size() * sizeof(cf32), hipMemcpyDeviceToHost));
         put(out, 202, all.data(), (int64_t)(all.size() * sizeof(cf32)));
@@ -158,7 +168,7 @@ int main(int argc, char **argv) {
         HIP_OK(hipFree((void *)d_in[r]));
         HIP_OK(hipFree(d_out[r]));
     }
-    HIP_OK(hipSetDevice(devs[0]));
+    HIP_OK(hipSetDevice(devs[root]));
     HIP_OK(hipFree(d_root));
     std::printf("sharded_main: %d channels x %zu samples over %d GPU(s) ok\n", C, n, R);
     return 0;

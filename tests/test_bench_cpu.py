@@ -55,3 +55,39 @@ def test_world_mismatch_fails_loudly():
 def test_host_cores_reports_share():
     n, note = bench.host_cores()
     assert n >= 1 and "machine nproc" in note
+
+
+def test_channel_layout_matches_baseline_configs():
+    """N = 1 is configs[1] (one 2^28 channel); N > 1 is configs[2]'s layout,
+    8 channels of 2^28 per GPU (64 over 8 GPUs) with a 32 GiB gather at N = 8."""
+    a = types.SimpleNamespace(workload="decim", samples=None, channels_per_gpu=None)
+    one = bench.channel_layout(a, 1)
+    assert one == {"channels_per_gpu": 1, "channels_total": 1, "samples_per_channel": 1 << 28, "gather_bytes": 0}
+    for n in (2, 4, 8):
+        lay = bench.channel_layout(a, n)
+        assert lay["channels_per_gpu"] == 8 and lay["channels_total"] == 8 * n
+        assert lay["gather_bytes"] == 8 * n * (1 << 26) * 8
+    assert bench.channel_layout(a, 8)["gather_bytes"] == 32 << 30
+    a.channels_per_gpu = 1
+    assert bench.channel_layout(a, 8)["channels_total"] == 8
+    c = types.SimpleNamespace(workload="corr", samples=1 << 26, channels_per_gpu=None)
+    assert bench.channel_layout(c, 8)["channels_per_gpu"] == 1 and bench.channel_layout(c, 8)["gather_bytes"] == 0
+
+
+def test_gpus8_dry_run_world_and_layout():
+    """`bench.py --gpus 8 --dry-run`, the driver's N = 8 command with no GPU
+    touched: 8 ranks assemble one gloo world, and every rank holds configs[2]'s
+    layout (8 x 2^28-sample channels per rank, 64 in all, 32 GiB gather)."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "1"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--dry-run"],
+                       capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert sorted(l["rank"] for l in lines) == list(range(8))
+    for l in lines:
+        assert l["world"] == 8 and l["world_seen"] == 8
+        assert l["layout"] == {"channels_per_gpu": 8, "channels_total": 64, "samples_per_channel": 1 << 28,
+                               "gather_bytes": 32 << 30}

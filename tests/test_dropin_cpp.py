@@ -244,3 +244,60 @@ def test_sharded_program_matches_oracle(tmp_path):
     assert got[200] == np.concatenate(alls).tobytes()
     assert got[201] == got[200]  # strided rows through the Memcpy2D branch of the gather
     assert got[202] == got[200]  # operator outliving its GpuComm
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ndebug", [False, True], ids=["assert", "NDEBUG"])
+@pytest.mark.parametrize("device", [False, True], ids=["host", "device"])
+def test_mixer_step_undersized_out_is_refused(tmp_path, ndebug, device):
+    """Mixer::step with out shorter than in (mixers.h:172-175
+    writes in.size() outputs regardless) asserts in a debug build and throws
+    std::length_error under NDEBUG -- before anything is staged or launched,
+    so nothing is written past out's end."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    src = r"""
+#include <csignal>
+#include <cstdio>
+#include <unistd.h>
+#include <hip/hip_runtime.h>
+#include "mixers.h"
+using ci16 = std::complex<int16_t>;
+// the assert's abort() ends the process with a plain exit status (9), not a
+// SIGABRT death, so the GPU box sees an ordinary exit
+extern "C" void on_abort(int) { _exit(9); }
+int main() {
+    std::signal(SIGABRT, on_abort);
+    dsptl::Mixer<ci16, ci16, int16_t, 4096> m;
+    m.reset(0.1f);
+    std::vector<ci16> in(1000, ci16(100, -100)), out(999);
+    try {
+        if (DEVICE) {
+            ci16 *din = nullptr, *dout = nullptr;
+            if (hipMalloc(&din, 1000 * sizeof(ci16)) || hipMalloc(&dout, 999 * sizeof(ci16))) return 3;
+            m.step(dsptl::DeviceSpan<const ci16>{din, 1000}, dsptl::DeviceSpan<ci16>{dout, 999});
+        } else {
+            m.step(in, out);
+        }
+    } catch (const std::length_error &e) {
+        std::printf("length_error: %s\n", e.what());
+        return 7;
+    }
+    std::printf("no error\n");
+    return 0;
+}
+"""
+    p = tmp_path / "t.cpp"
+    p.write_text(src)
+    exe = str(tmp_path / "t")
+    cmd = ["g++", "-std=c++14", "-O1", "-D__HIP_PLATFORM_AMD__", f"-DDEVICE={int(device)}", "-I", INC,
+           "-I", "/opt/rocm/include", str(p), "-o", exe, "-L", LIBDIR, "-lsrcdsp_hip", "-L/opt/rocm/lib",
+           "-lamdhip64", f"-Wl,-rpath,{LIBDIR}", "-Wl,-rpath,/opt/rocm/lib"] + (["-DNDEBUG"] if ndebug else [])
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    if ndebug:
+        assert r.returncode == 7 and "output buffer smaller" in r.stdout, (r.returncode, r.stdout, r.stderr)
+    else:
+        assert r.returncode == 9 and "output buffer smaller than the call writes" in r.stderr, (r.returncode, r.stderr)

@@ -80,3 +80,30 @@ def test_two_ranks_on_gpu_match_single_process(tmp_path, pat_at):
     go.set_pattern(p)
     ofound, oidx = go.step(xc)
     assert ofound == found and (not found or oidx == idx)
+
+
+def test_bench_two_rank_rehearsal_default_layout():
+    """`bench.py --gpus 2` as the driver runs it, both ranks on cuda:0
+    (collectives rehearsed over gloo: two ranks on one device cannot form an
+    RCCL communicator): the default N > 1 layout is configs[2]'s, 8 channels
+    of 2^28 samples per rank, and the timed gather moves all 16 channels'
+    outputs (8 GiB) to rank 0."""
+    import json
+    import torch
+    if torch.cuda.device_count() < 1:
+        pytest.skip("no GPU")
+    root = os.path.dirname(HERE)
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["SRCDSP_BENCH_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "3",
+                        "--warmup", "1", "--no-cpu-baseline", "--no-pcie"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["world_size_reported"] == 2 and line["backend"] == "gloo"
+    cfg = line["config"]
+    assert cfg["channels_per_gpu"] == 8 and cfg["channels_total"] == 16 and cfg["baseline_config"] == "configs[2]"
+    assert cfg["samples_per_channel"] == 1 << 28
+    assert line["gather_bytes"] == 16 * (1 << 26) * 8 and line["gather_ms"] > 0
+    assert line["roofline"]["per_gpu"] and line["roofline"]["channels_per_launch"] == 8
+    assert line["roofline"]["algorithmic_bytes_per_launch"] == 8 * (1 << 28) * 10
