@@ -15,6 +15,7 @@
 #                    for each tap count of ${WP_TAPS} (default 127)
 #   phase            per-phase cycles of the config-4 kernel (scripts/tune/phase_clock.py; tuning build
 #                    scripts/tune/ab/libsrcdsp_hip_phase.so)
+#   pmcw             SQ/LDS counter passes (scripts/tune/pmc_workload.py) for each WORKLOAD:KERNEL of ${PMCW}
 #   envelope         scripts/shape_envelope.py ${ENV_M}
 #   census           workgroup placement census (scripts/tune/census.py)
 #   ab               same-box A/B of scripts/tune/ab/libsrcdsp_hip_base.so vs the tree's library
@@ -64,6 +65,11 @@ for s in ${STEPS:-smoke tests bench}; do
       done ;;
     phase) SRCDSP_HIP_LIB=$PWD/scripts/tune/ab/libsrcdsp_hip_phase.so \
              step phase_$TAG 120 python3 -u scripts/tune/phase_clock.py ${PHASE_WL:-mixdecim} ;;
+    pmcw)
+      for wk in ${PMCW:-mixdecim:decim_dot2_ci16}; do
+        w=${wk%%:*}; k=${wk#*:}
+        step pmcw_${w}_$TAG 300 python -u scripts/tune/pmc_workload.py gpurun_out/pmcw_${w}_$TAG.json $w $k
+      done ;;
     envelope) step envelope_$TAG 600 python -u scripts/shape_envelope.py ${ENV_M} ;;
     census) step census_$TAG 120 python -u scripts/tune/census.py ;;
     ab) step ab_$TAG 1000 bash scripts/tune/ab_libs.sh ;;

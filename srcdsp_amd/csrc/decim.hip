@@ -116,7 +116,7 @@ int launch_ci16_dot2_shape(DecimLaunch L, int channels, bool mixed, hipStream_t 
         const unsigned long N = L.mix_N, h = (unsigned long)dot2_rt_halo(L.ntaps) % N;
         L.mix_phase_tile0 = (unsigned)((L.mix_phase0 + ((N - h) % N) * L.mix_freq) % N);
     }
-    if (mixed && TABM == 2) {
+    if (mixed && TABM >= 2) {
         L.mix_pe = mixer_seq_period(L.mix_N, L.mix_freq);
         L.mix_pe_dtile = (unsigned)((unsigned long)SPT % L.mix_pe);
         L.mix_pe_drow = (unsigned)((4ul * BLOCK) % L.mix_pe);
@@ -147,8 +147,12 @@ int launch_ci16_dot2(DecimLaunch L, int channels, bool mixed, hipStream_t s) {
     // doubled phase table (only these instantiations are compiled outside the
     // tuning build)
     constexpr int BLOCK = MD == 1 ? 256 : 512;  // M = 1: 3 workgroups of 4 waves per CU
-    if (mixed && mixer_seq_period(L.mix_N, L.mix_freq) > kSeqMax)
-        return launch_ci16_dot2_shape<NT, BLOCK, 1, MD>(L, channels, mixed, s);
+    if (!mixed) return launch_ci16_dot2_shape<NT, BLOCK, 2, MD>(L, channels, mixed, s);
+    const unsigned pe = mixer_seq_period(L.mix_N, L.mix_freq);
+    if (pe > kSeqMax) return launch_ci16_dot2_shape<NT, BLOCK, 1, MD>(L, channels, mixed, s);
+#ifndef SRCDSP_NO_SEQ2
+    if (pe <= (unsigned)kSeq2Max) return launch_ci16_dot2_shape<NT, BLOCK, 3, MD>(L, channels, mixed, s);
+#endif
     return launch_ci16_dot2_shape<NT, BLOCK, 2, MD>(L, channels, mixed, s);
 }
 

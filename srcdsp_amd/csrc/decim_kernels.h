@@ -1376,10 +1376,16 @@ __global__ __launch_bounds__(kDtBlock) void decim_tile(DecimLaunch a) {
 //    gcd(freq, N), 4); sample s's phase (phi0 + s*freq) mod N depends on s mod
 //    Pe only), stored twice (2 Pe words).  A lane's 4 samples are 4
 //    consecutive words: one conflict-free ds_read_b128 per granule, any freq.
+//  3 (two-word sequence table, Pe <= kSeq2Max): as 2, but both dot2 operands
+//    of each sample are stored, A = (lr, -li) in one table and B = (li, lr)
+//    in a second one kSeq2Off words further: re = dot2(x, A), im = dot2(x, B)
+//    with no negate or half swap per sample (two conflict-free ds_read_b128
+//    per granule).  |lr|, |li| <= 16383 (the LUT's amplitude), so -li fits.
 // Products via VOP3 dot2 and the pair clamp above.
+constexpr int kSeq2Off = 4096, kSeq2Max = kSeq2Off / 2;
 template <int NT, int BLOCK, bool MIX, int MINW, int TABM = 0, int MD = 4>
 __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
-    constexpr bool TAB2 = TABM == 1, SEQT = TABM == 2;
+    constexpr bool TAB2 = TABM == 1, SEQT = TABM == 2 || TABM == 3, SEQ2 = TABM == 3;
     constexpr bool RT = NT == 0;                  // the tap count at run time (a.ntaps <= kDot2MaxTaps)
     static_assert(MD == 1 || MD == 2 || MD == 4 || MD == 8 || MD == 16, "M dividing the 16-sample lane chunk");
     static_assert(MD == 4 || RT, "tap counts are compiled in at M = 4 only");
@@ -1441,7 +1447,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
             }
             unsigned ic = k + N / 4;
             ic = ic >= N ? ic - N : ic;
-            ctab[i] = ((uint32_t)(uint16_t)tab[ic]) | ((uint32_t)(uint16_t)tab[k] << 16);
+            if constexpr (SEQ2) {  // A = (lr, -li), B = (li, lr)
+                ctab[i] = ((uint32_t)(uint16_t)tab[ic]) | ((uint32_t)(uint16_t)(-tab[k]) << 16);
+                ctab[kSeq2Off + i] = ((uint32_t)(uint16_t)tab[k]) | ((uint32_t)(uint16_t)tab[ic] << 16);
+            } else {
+                ctab[i] = ((uint32_t)(uint16_t)tab[ic]) | ((uint32_t)(uint16_t)tab[k] << 16);
+            }
         }
         __syncthreads();
     }
@@ -1449,7 +1460,12 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     auto phase_add = [&](unsigned base, unsigned k) { return (base + (k % N) * fr) % N; };
     auto mix1 = [&](uint32_t w, unsigned ph) {
         int32_t re, im;
-        mix_dot2(w, ctab[ph], re, im);
+        if constexpr (SEQ2) {
+            re = clamp_s14(sdot2(w, ctab[ph], 0));
+            im = clamp_s14(sdot2(w, ctab[kSeq2Off + ph], 0));
+        } else {
+            mix_dot2(w, ctab[ph], re, im);
+        }
         return pack16(re, im);
     };
     // input sample s >= 0 of this call, mixed (any table form)
@@ -1473,6 +1489,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
         return (a.mix_phase_tile0 + ((unsigned)(tile % N)) * a.mix_dtile) % N;
     };
 
+    // staged granule of round i (one 16-B granule per lane per round), -1 past the tile
+    auto sg = [&](int i) { const int g = t + i * BLOCK; return g < TG ? g : -1; };
     uint4 v[PER];
     auto stage_load = [&](long tile) {  // tile >= 1
         const long b0 = (long)SPT * tile - HS;
@@ -1481,8 +1499,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
         __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)(in + b0), 0, nrec, 0x00020000);
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
-            const int g = t + i * BLOCK;
-            if (g < TG) {
+            const int g = sg(i);
+            if (g >= 0) {
                 auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * g, 0, 0);
                 v[i] = make_uint4(w[0], w[1], w[2], w[3]);
             }
@@ -1521,10 +1539,24 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     // SEQT: the granule's 4 words at ctab[m + lane offset], m = (first staged
     // sample of the granule row) mod Pe (uniform); lane offset 4t mod Pe
     const unsigned lo_t = SEQT ? (4u * t) % Pe : 0u;
-    auto put_mixed_seq = [&](int g, uint4 w, unsigned m) {
-        // m + lo_t is a multiple of 4 words: one 16-B read (the compiler, not
+    auto put_mixed_seq2 = [&](int g, uint4 w, unsigned m, unsigned lo) {
+        const uint4 A = *(const uint4 *)__builtin_assume_aligned(&ctab[m + lo], 16);
+        const uint4 B = *(const uint4 *)__builtin_assume_aligned(&ctab[kSeq2Off + m + lo], 16);
+        const int32_t r0 = sdot2_0(w.x, A.x), i0 = sdot2_0(w.x, B.x);
+        const int32_t r1 = sdot2_0(w.y, A.y), i1 = sdot2_0(w.y, B.y);
+        const int32_t r2 = sdot2_0(w.z, A.z), i2 = sdot2_0(w.z, B.z);
+        const int32_t r3 = sdot2_0(w.w, A.w), i3 = sdot2_0(w.w, B.w);
+        *lds_half(g, 0) = make_uint2(clamp_pair_s14(r0, r1), clamp_pair_s14(r2, r3));
+        *lds_half(g, 1) = make_uint2(clamp_pair_s14(i0, i1), clamp_pair_s14(i2, i3));
+    };
+    auto put_mixed_seq = [&](int g, uint4 w, unsigned m, unsigned lo) {
+        if constexpr (SEQ2) {
+            put_mixed_seq2(g, w, m, lo);
+            return;
+        }
+        // m + lo is a multiple of 4 words: one 16-B read (the compiler, not
         // knowing that, would split it into 4-way-conflicting ds_read2_b32)
-        const uint4 c = *(const uint4 *)__builtin_assume_aligned(&ctab[m + lo_t], 16);
+        const uint4 c = *(const uint4 *)__builtin_assume_aligned(&ctab[m + lo], 16);
         auto neg_hi = [](uint32_t x) {
             return __builtin_bit_cast(uint32_t, __builtin_bit_cast(short2_t_, x) * (short2_t_){1, -1});
         };
@@ -1559,9 +1591,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
             const long b0 = -HS;
 #pragma unroll
             for (int i = 0; i < PER; ++i) {
-                const int g = t + i * BLOCK;
+                const int g = sg(i);
                 const long s0 = b0 + 4 * (long)g;
-                if (g < TG) {
+                if (g >= 0) {
                     uint32_t w[4];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
@@ -1586,8 +1618,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
             unsigned m = m_tile;  // wave-uniform
 #pragma unroll
             for (int i = 0; i < PER; ++i) {
-                const int g = t + i * BLOCK;
-                if (g < TG) put_mixed_seq(g, v[i], m);
+                const int g = sg(i);
+                if (g >= 0) put_mixed_seq(g, v[i], m, lo_t);
                 m = advp(m, a.mix_pe_drow);
             }
         } else if (MIX && TAB2 && tile != 0) {
@@ -1609,8 +1641,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
         } else {
 #pragma unroll
             for (int i = 0; i < PER; ++i) {
-                const int g = t + i * BLOCK;
-                if (g < TG) put(g, v[i].x, v[i].y, v[i].z, v[i].w);
+                const int g = sg(i);
+                if (g >= 0) put(g, v[i].x, v[i].y, v[i].z, v[i].w);
             }
         }
         SRCDSP_PH(ph2);
@@ -1659,7 +1691,20 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
             load_g(1);
 #pragma unroll
             for (int j = 0; j < JC; ++j) {
+#ifdef SRCDSP_TUNE_HALF_LDS
+                // tuning probe only (wrong outputs): every other window
+                // granule is an opaque register value instead of an LDS read,
+                // so the tap loop issues the same VALU work with half the
+                // ds_read_b128 -- the price of the window reads
+                if ((j & 3) == 1 && ((j >> 2) & 1)) {
+                    const int c = -1 - (j >> 2);
+                    for (int k = 0; k < 4; ++k) asm volatile("" : "=v"(Dr[OFF + 4 * c + k]), "=v"(Di[OFF + 4 * c + k]));
+                } else if ((j & 3) == 1) {
+                    load_g(-1 - (j >> 2));
+                }
+#else
                 if ((j & 3) == 1) load_g(-1 - (j >> 2));
+#endif
                 if ((j & 15) == 0) asm volatile("" : "+s"(tp));
                 const uint32_t P = tp[j];
 #pragma unroll
