@@ -88,12 +88,17 @@ public:
     /// dnsampling_filters.h:129-172 for every channel: input[ch] -> filteredSignal[ch],
     /// each output vector pre-sized to input[ch].size()/M (all channels the same length)
     void step(const std::vector<std::vector<InType>> &input, std::vector<std::vector<OutType>> &filteredSignal) {
-        assert((int)input.size() == channels_ && (int)filteredSignal.size() == channels_);
+        // the C ABI takes one length for every channel and no output sizes:
+        // every vector is checked here (throws under NDEBUG) before any is touched
+        srcdsp_detail::check_shape((int)input.size() == channels_ && (int)filteredSignal.size() == channels_,
+                                  "ShardedDnsamplingFir::step: one input and one output vector per channel");
         std::vector<const void *> in(channels_);
         std::vector<void *> out(channels_);
         for (int ch = 0; ch < channels_; ++ch) {
-            assert(input[ch].size() == input[0].size());
-            assert(filteredSignal[ch].size() * M == input[ch].size());
+            srcdsp_detail::check_shape(input[ch].size() == input[0].size(),
+                                      "ShardedDnsamplingFir::step: channels of different lengths");
+            srcdsp_detail::check_shape(filteredSignal[ch].size() * M == input[ch].size(),
+                                      "ShardedDnsamplingFir::step: output vector != input size / M");
             in[ch] = input[ch].data();
             out[ch] = filteredSignal[ch].data();
         }
@@ -104,7 +109,8 @@ public:
     /// rows in_stride / out_stride samples apart; asynchronous on the comm streams
     void step(const std::vector<const InType *> &d_in, size_t in_stride, const std::vector<OutType *> &d_out,
               size_t out_stride, size_t n_in) {
-        assert((int)d_in.size() == ranks_ && (int)d_out.size() == ranks_);
+        srcdsp_detail::check_shape((int)d_in.size() == ranks_ && (int)d_out.size() == ranks_,
+                                  "ShardedDnsamplingFir::step(device): one input and one output pointer per rank");
         std::vector<const void *> i(d_in.begin(), d_in.end());
         std::vector<void *> o(d_out.begin(), d_out.end());
         srcdsp_detail::check(srcdsp_decim_sharded_step(h_, i.data(), in_stride, o.data(), out_stride, n_in),
@@ -112,6 +118,7 @@ public:
     }
     /// every channel's n_out outputs to d_root (rank root's GPU), channel-major
     void gather(const std::vector<OutType *> &d_out, size_t out_stride, size_t n_out, OutType *d_root, int root = 0) {
+        srcdsp_detail::check_shape((int)d_out.size() == ranks_, "ShardedDnsamplingFir::gather: one pointer per rank");
         std::vector<void *> o(d_out.begin(), d_out.end());
         srcdsp_detail::check(srcdsp_decim_sharded_gather(h_, o.data(), out_stride, n_out, d_root, root),
                              "ShardedDnsamplingFir::gather");

@@ -52,6 +52,14 @@ inline void check_size(bool ok, const char *what) {
     if (!ok) throw std::length_error(std::string(what) + ": output buffer smaller than the input");
 }
 
+/// Vector shapes a call needs but the C ABI cannot check (one length for all
+/// channels, no output sizes): asserts, and with NDEBUG throws
+/// std::length_error before anything is copied or launched.
+inline void check_shape(bool ok, const char *what) {
+    assert(ok && "buffer shapes do not match the call");
+    if (!ok) throw std::length_error(what);
+}
+
 template <class T> struct kind;  // sample / coefficient type codes
 template <> struct kind<std::complex<float>> { static constexpr int v = 0; };
 template <> struct kind<std::complex<int16_t>> { static constexpr int v = 1; };

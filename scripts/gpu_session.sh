@@ -8,8 +8,11 @@
 #   tests            pytest -m gpu (PYTEST_K: -k filter)
 #   bench            bench.py ${BENCH_ARGS} (default: the headline, driver protocol --steps 20 --warmup 5)
 #   bench_all        every workload's bench line (steady protocol)
+#   bench_cold       every workload's line under the driver's protocol (--warmup 5 --steps 20), IDLE s apart
 #   prof             rocprofv3 --kernel-trace --stats of bench.py ${BENCH_ARGS} (per-dispatch CSV kept)
 #   pmc              FETCH_SIZE / WRITE_SIZE passes (scripts/pmc_traffic.py) for each of ${PMC_WORKLOADS}
+#                    (decimx8 = the headline's 8-channel batched step, config 3's per-GPU share);
+#                    merge into profiles/pmc_traffic.json with scripts/merge_pmc.py TAG
 #   ramp             cold ramps of tune variants ${VARIANTS} (scripts/tune/ramp.py), IDLE s apart
 #   wpower           socket power / clock / limiter counters through a cold start (scripts/tune/window_power.py)
 #                    for each tap count of ${WP_TAPS} (default 127)
@@ -46,11 +49,20 @@ for s in ${STEPS:-smoke tests bench}; do
       for w in decim mixdecim ci16decim corr fir up; do
         step bench_${w}_$TAG 300 python -u bench.py --workload $w --no-cpu-baseline --no-pcie
       done ;;
+    bench_cold)  # the driver's protocol for every workload, each a fresh process after ${IDLE:-8} s idle
+      for w in decim mixdecim ci16decim corr fir up; do
+        sleep ${IDLE:-8}
+        step benchcold_${w}_$TAG 300 python -u bench.py --workload $w --no-cpu-baseline --no-pcie --warmup 5 --steps 20
+      done ;;
     prof) step prof_$TAG 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv \
             -- python3 bench.py --no-cpu-baseline --no-pcie ${BENCH_ARGS:---steps 20 --warmup 5} ;;
     pmc)
       for w in ${PMC_WORKLOADS:-decim}; do
-        step pmc_${w}_$TAG 600 python -u scripts/pmc_traffic.py --workload $w --tag $TAG
+        if [ "$w" = decimx8 ]; then
+          step pmc_${w}_$TAG 600 python -u scripts/pmc_traffic.py --workload decim --channels 8 --tag $TAG
+        else
+          step pmc_${w}_$TAG 600 python -u scripts/pmc_traffic.py --workload $w --tag $TAG
+        fi
       done ;;
     ramp)
       : > gpurun_out/ramp_$TAG.jsonl

@@ -301,3 +301,58 @@ int main() {
         assert r.returncode == 7 and "output buffer smaller" in r.stdout, (r.returncode, r.stdout, r.stderr)
     else:
         assert r.returncode == 9 and "output buffer smaller than the call writes" in r.stderr, (r.returncode, r.stderr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ndebug", [False, True], ids=["assert", "NDEBUG"])
+@pytest.mark.parametrize("case", ["short_out", "ragged_in", "few_vectors"])
+def test_sharded_step_bad_vectors_are_refused(tmp_path, ndebug, case):
+    """ShardedDnsamplingFir::step(host vectors): the C ABI takes one length for
+    every channel and no output sizes, so the wrapper checks every vector
+    first -- an output of the wrong size, channels of different lengths, or
+    fewer vectors than channels assert in a debug build and throw
+    std::length_error under NDEBUG, before anything is copied or launched."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    src = r"""
+#include <csignal>
+#include <cstdio>
+#include <unistd.h>
+#include <hip/hip_runtime.h>
+#include "sharded_filters.h"
+using cf32 = std::complex<float>;
+extern "C" void on_abort(int) { _exit(9); }
+int main() {
+    std::signal(SIGABRT, on_abort);
+    dsptl::GpuComm comm(std::vector<int>{0});
+    std::vector<float> taps(127, 0.01f);
+    dsptl::ShardedDnsamplingFir<cf32, cf32, cf32, float, 4> f(comm, 3, taps);
+    std::vector<std::vector<cf32>> in(3, std::vector<cf32>(4096)), out(3, std::vector<cf32>(1024));
+    if (CASE == 0) out[2].resize(1023);
+    if (CASE == 1) in[1].resize(4100);
+    if (CASE == 2) { in.resize(2); out.resize(2); }
+    try {
+        f.step(in, out);
+    } catch (const std::length_error &e) {
+        std::printf("length_error: %s\n", e.what());
+        return 7;
+    }
+    std::printf("no error\n");
+    return 0;
+}
+"""
+    p = tmp_path / "t.cpp"
+    p.write_text(src)
+    exe = str(tmp_path / "t")
+    icase = ["short_out", "ragged_in", "few_vectors"].index(case)
+    cmd = ["g++", "-std=c++14", "-O1", "-D__HIP_PLATFORM_AMD__", f"-DCASE={icase}", "-I", INC,
+           "-I", "/opt/rocm/include", str(p), "-o", exe, "-L", LIBDIR, "-lsrcdsp_hip", "-L/opt/rocm/lib",
+           "-lamdhip64", f"-Wl,-rpath,{LIBDIR}", "-Wl,-rpath,/opt/rocm/lib"] + (["-DNDEBUG"] if ndebug else [])
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    if ndebug:
+        assert r.returncode == 7 and "ShardedDnsamplingFir::step" in r.stdout, (r.returncode, r.stdout, r.stderr)
+    else:
+        assert r.returncode == 9 and "buffer shapes do not match the call" in r.stderr, (r.returncode, r.stderr)
