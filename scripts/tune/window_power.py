@@ -3,7 +3,11 @@
 through the driver's window (launches 6-25 of a cold start) of the headline
 (tuning only; read-only amdsmi queries, no setting touched).
 
-  python scripts/tune/window_power.py [LAUNCHES] [IDLE_S] [TAPS]
+  python scripts/tune/window_power.py [LAUNCHES] [IDLE_S] [TAPS | w:WORKLOAD]
+
+TAPS: the headline at M = 4 with an n-tap filter (default 127); w:WORKLOAD: one
+step of a bench.py workload instead (w:mixdecim, w:ci16decim, w:up, w:corr,
+w:fir, w:decim).
 
 One fresh process: build the headline operator, idle IDLE_S seconds (default
 8), then LAUNCHES (default 300) back-to-back FilterDnsamplingFir.step() calls
@@ -84,15 +88,26 @@ def violation(h):
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 300
     idle_s = float(sys.argv[2]) if len(sys.argv) > 2 else 8.0
-    taps = int(sys.argv[3]) if len(sys.argv) > 3 else 127
+    arg = sys.argv[3] if len(sys.argv) > 3 else "127"
     amdsmi.amdsmi_init()
     h = amdsmi.amdsmi_get_processor_handles()[0]
-    L = 1 << 28
-    x = torch.empty(L, dtype=torch.complex64, device="cuda")
-    S.fill_synthetic(x, "cf32")
-    y = torch.empty(L // 4, dtype=torch.complex64, device="cuda")
-    f = S.FilterDnsamplingFir(hamming_sinc(taps), 4)
-    f.step(x[: 1 << 16], y[: 1 << 14])  # load the code object; negligible work
+    if arg.startswith("w:"):
+        import bench
+        wl = arg[2:]
+        L = (1 << 26) if wl == "corr" else (1 << 28)
+        work = bench.WORKLOADS[wl](S, torch, L, 1, 0, "fma")
+        step = work.step
+        step()  # code objects loaded before the idle pause
+        taps = wl
+    else:
+        taps = int(arg)
+        L = 1 << 28
+        x = torch.empty(L, dtype=torch.complex64, device="cuda")
+        S.fill_synthetic(x, "cf32")
+        y = torch.empty(L // 4, dtype=torch.complex64, device="cuda")
+        f = S.FilterDnsamplingFir(hamming_sinc(taps), 4)
+        f.step(x[: 1 << 16], y[: 1 << 14])  # load the code object; negligible work
+        step = lambda: f.step(x, y)  # noqa: E731
     torch.cuda.synchronize()
     recs, stop = [], threading.Event()
     th = threading.Thread(target=sampler, args=(h, recs, stop), daemon=True)
@@ -109,7 +124,7 @@ def main():
     torch.cuda._sleep(int(2e8))
     for a, b in ev:
         a.record()
-        f.step(x, y)
+        step()
         b.record()
     torch.cuda.synchronize()
     t_end = time.perf_counter()

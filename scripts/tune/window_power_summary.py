@@ -29,7 +29,7 @@ def summarise(path):
             prev = k
     out = [f"# {path}: {len(ms)} launches, first at {st[0]:.1f} ms, last ends at {st[-1] + ms[-1]:.1f} ms",
            "# launches 1-25 ms: " + " ".join(f"{v:.3f}" for v in ms[:25]),
-           "interval_ms        launches  mean_ms  power_W  ppt_active  gfxclk_MHz  avg_pwr_reported_W"]
+           "interval_ms        launches  mean_ms  power_W  mJ/launch  ppt_active  gfxclk_MHz  avg_pwr_reported_W"]
     for a, b in zip(upd, upd[1:]):
         t0, t1 = a["rel_ms"], b["rel_ms"]
         dacc = b["accumulation_counter"] - a["accumulation_counter"]
@@ -40,7 +40,10 @@ def summarise(path):
         ls = [i for i, s in enumerate(st) if t0 <= s < t1]
         lr = f"{ls[0] + 1}-{ls[-1] + 1}" if ls else "-"
         mm = f"{sum(ms[i] for i in ls) / len(ls):.4f}" if ls else "-"
-        out.append(f"{t0:7.1f}-{t1:7.1f}  {lr:>9}  {mm:>7}  {p:7.0f}  {ppt:10.2f}  {b['current_gfxclk']:10.0f}"
+        # energy per launch where launches fill the interval back to back
+        full = ls and st[ls[0]] - t0 < 1.0 and st[ls[-1]] + ms[ls[-1]] > t1 - 1.0
+        mj = f"{p * sum(ms[i] for i in ls) / len(ls) * 1e-3 * 1e3:.1f}" if full else "-"
+        out.append(f"{t0:7.1f}-{t1:7.1f}  {lr:>9}  {mm:>7}  {p:7.0f}  {mj:>9}  {ppt:10.2f}  {b['current_gfxclk']:10.0f}"
                    f"  {b['current_socket_power']:8.0f}")
     return "\n".join(out)
 
