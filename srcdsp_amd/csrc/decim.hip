@@ -150,10 +150,15 @@ int launch_ci16_dot2(DecimLaunch L, int channels, bool mixed, hipStream_t s) {
     if (!mixed) return launch_ci16_dot2_shape<NT, BLOCK, 2, MD>(L, channels, mixed, s);
     const unsigned pe = mixer_seq_period(L.mix_N, L.mix_freq);
     if (pe > kSeqMax) return launch_ci16_dot2_shape<NT, BLOCK, 1, MD>(L, channels, mixed, s);
-#ifndef SRCDSP_NO_SEQ2
+    // two-word sequence tables: stored twice up to Pe = 2048, once (index
+    // wrapped) up to 4096 -- config 4's mixer (N = 4096, f = 0.1: freq word
+    // 205, Pe = 4096) takes the latter
     if (pe <= (unsigned)kSeq2Max) return launch_ci16_dot2_shape<NT, BLOCK, 3, MD>(L, channels, mixed, s);
-#endif
+#ifdef SRCDSP_SEQ_ONEWORD
     return launch_ci16_dot2_shape<NT, BLOCK, 2, MD>(L, channels, mixed, s);
+#else
+    return launch_ci16_dot2_shape<NT, BLOCK, 4, MD>(L, channels, mixed, s);
+#endif
 }
 
 template <int KV>

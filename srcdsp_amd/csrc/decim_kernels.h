@@ -1381,11 +1381,14 @@ __global__ __launch_bounds__(kDtBlock) void decim_tile(DecimLaunch a) {
 //    in a second one kSeq2Off words further: re = dot2(x, A), im = dot2(x, B)
 //    with no negate or half swap per sample (two conflict-free ds_read_b128
 //    per granule).  |lr|, |li| <= 16383 (the LUT's amplitude), so -li fits.
+//  4 (two-word sequence table stored once, Pe <= kSeq2Off): as 3 with each
+//    table held once (2 Pe words: the LDS of form 2's doubled one-word table),
+//    the granule's index m + lo (< 2 Pe) wrapped by one subtract and one min.
 // Products via VOP3 dot2 and the pair clamp above.
 constexpr int kSeq2Off = 4096, kSeq2Max = kSeq2Off / 2;
 template <int NT, int BLOCK, bool MIX, int MINW, int TABM = 0, int MD = 4>
 __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
-    constexpr bool TAB2 = TABM == 1, SEQT = TABM == 2 || TABM == 3, SEQ2 = TABM == 3;
+    constexpr bool TAB2 = TABM == 1, SEQT = TABM >= 2, SEQ2 = TABM >= 3, SEQ1 = TABM == 4;
     constexpr bool RT = NT == 0;                  // the tap count at run time (a.ntaps <= kDot2MaxTaps)
     static_assert(MD == 1 || MD == 2 || MD == 4 || MD == 8 || MD == 16, "M dividing the 16-sample lane chunk");
     static_assert(MD == 4 || RT, "tap counts are compiled in at M = 4 only");
@@ -1436,7 +1439,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     const unsigned Pe = SEQT ? a.mix_pe : 1u;
     if constexpr (MIX) {
         const int16_t *tab = a.mix_table;
-        const int nw = SEQT ? 2 * (int)Pe : (TAB2 ? 2 : 1) * (int)N;
+        const int nw = SEQ1 ? (int)Pe : SEQT ? 2 * (int)Pe : (TAB2 ? 2 : 1) * (int)N;
         for (int i = t; i < nw; i += BLOCK) {
             unsigned k;
             if constexpr (SEQT) {
@@ -1540,8 +1543,13 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     // sample of the granule row) mod Pe (uniform); lane offset 4t mod Pe
     const unsigned lo_t = SEQT ? (4u * t) % Pe : 0u;
     auto put_mixed_seq2 = [&](int g, uint4 w, unsigned m, unsigned lo) {
-        const uint4 A = *(const uint4 *)__builtin_assume_aligned(&ctab[m + lo], 16);
-        const uint4 B = *(const uint4 *)__builtin_assume_aligned(&ctab[kSeq2Off + m + lo], 16);
+        unsigned ix = m + lo;  // < 2 Pe; a multiple of 4 words
+        if constexpr (SEQ1) {
+            const unsigned jx = ix - Pe;
+            ix = jx < ix ? jx : ix;  // ix mod Pe (v_sub + v_min)
+        }
+        const uint4 A = *(const uint4 *)__builtin_assume_aligned(&ctab[ix], 16);
+        const uint4 B = *(const uint4 *)__builtin_assume_aligned(&ctab[kSeq2Off + ix], 16);
         const int32_t r0 = sdot2_0(w.x, A.x), i0 = sdot2_0(w.x, B.x);
         const int32_t r1 = sdot2_0(w.y, A.y), i1 = sdot2_0(w.y, B.y);
         const int32_t r2 = sdot2_0(w.z, A.z), i2 = sdot2_0(w.z, B.z);
