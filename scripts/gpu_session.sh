@@ -9,6 +9,7 @@
 #   bench            bench.py ${BENCH_ARGS} (default: the headline, driver protocol --steps 20 --warmup 5)
 #   bench_all        every workload's bench line (steady protocol)
 #   bench_cold       every workload's line under the driver's protocol (--warmup 5 --steps 20), IDLE s apart
+#   bench8           config 3's per-GPU share (--channels-per-gpu 8), driver protocol and steady
 #   prof             rocprofv3 --kernel-trace --stats of bench.py ${BENCH_ARGS} (per-dispatch CSV kept)
 #   pmc              FETCH_SIZE / WRITE_SIZE passes (scripts/pmc_traffic.py) for each of ${PMC_WORKLOADS}
 #                    (decimx8 = the headline's 8-channel batched step, config 3's per-GPU share);
@@ -49,6 +50,9 @@ for s in ${STEPS:-smoke tests bench}; do
       for w in decim mixdecim ci16decim corr fir up; do
         step bench_${w}_$TAG 300 python -u bench.py --workload $w --no-cpu-baseline --no-pcie
       done ;;
+    bench8)  # config 3's per-GPU share (8 x 2^28 channels per step): driver protocol, then steady
+      step bench8cold_$TAG 300 python -u bench.py --channels-per-gpu 8 --warmup 5 --steps 20 --no-cpu-baseline --no-pcie
+      step bench8_$TAG 300 python -u bench.py --channels-per-gpu 8 --warmup 20 --steps 50 --no-cpu-baseline --no-pcie ;;
     bench_cold)  # the driver's protocol for every workload, each a fresh process after ${IDLE:-8} s idle
       for w in decim mixdecim ci16decim corr fir up; do
         sleep ${IDLE:-8}

@@ -142,10 +142,10 @@ int launch_ci16_dot2(DecimLaunch L, int channels, bool mixed, hipStream_t s) {
     default: break;
     }
 #endif
-    // the product shape: 512 lanes; the sequence mixer table (conflict-free
-    // reads for any frequency) when its period fits the LDS budget, else the
-    // doubled phase table (only these instantiations are compiled outside the
-    // tuning build)
+    // the product shape: 512 lanes; the two-word sequence mixer table
+    // (conflict-free reads for any frequency, no per-sample negate or swap)
+    // when its period fits the LDS budget, else the doubled phase table
+    // (only these instantiations are compiled outside the tuning build)
     constexpr int BLOCK = MD == 1 ? 256 : 512;  // M = 1: 3 workgroups of 4 waves per CU
     if (!mixed) return launch_ci16_dot2_shape<NT, BLOCK, 2, MD>(L, channels, mixed, s);
     const unsigned pe = mixer_seq_period(L.mix_N, L.mix_freq);
@@ -154,11 +154,7 @@ int launch_ci16_dot2(DecimLaunch L, int channels, bool mixed, hipStream_t s) {
     // wrapped) up to 4096 -- config 4's mixer (N = 4096, f = 0.1: freq word
     // 205, Pe = 4096) takes the latter
     if (pe <= (unsigned)kSeq2Max) return launch_ci16_dot2_shape<NT, BLOCK, 3, MD>(L, channels, mixed, s);
-#ifdef SRCDSP_SEQ_ONEWORD
-    return launch_ci16_dot2_shape<NT, BLOCK, 2, MD>(L, channels, mixed, s);
-#else
     return launch_ci16_dot2_shape<NT, BLOCK, 4, MD>(L, channels, mixed, s);
-#endif
 }
 
 template <int KV>

@@ -1557,11 +1557,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
         *lds_half(g, 0) = make_uint2(clamp_pair_s14(r0, r1), clamp_pair_s14(r2, r3));
         *lds_half(g, 1) = make_uint2(clamp_pair_s14(i0, i1), clamp_pair_s14(i2, i3));
     };
-    auto put_mixed_seq = [&](int g, uint4 w, unsigned m, unsigned lo) {
-        if constexpr (SEQ2) {
-            put_mixed_seq2(g, w, m, lo);
-            return;
-        }
+    auto put_mixed_seq1 = [&](int g, uint4 w, unsigned m, unsigned lo) {
         // m + lo is a multiple of 4 words: one 16-B read (the compiler, not
         // knowing that, would split it into 4-way-conflicting ds_read2_b32)
         const uint4 c = *(const uint4 *)__builtin_assume_aligned(&ctab[m + lo], 16);
@@ -1575,6 +1571,10 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
         const int32_t r3 = sdot2_0(w.w, neg_hi(c.w)), i3 = sdot2_0(swp(w.w), c.w);
         *lds_half(g, 0) = make_uint2(clamp_pair_s14(r0, r1), clamp_pair_s14(r2, r3));
         *lds_half(g, 1) = make_uint2(clamp_pair_s14(i0, i1), clamp_pair_s14(i2, i3));
+    };
+    auto put_mixed_seq = [&](int g, uint4 w, unsigned m, unsigned lo) {
+        if constexpr (SEQ2) put_mixed_seq2(g, w, m, lo);
+        else put_mixed_seq1(g, w, m, lo);
     };
     auto advp = [&](unsigned p, unsigned d) { p += d; const unsigned q = p - Pe; return q < p ? q : p; };
     // SEQT: (4*tile*TO - HS) mod Pe of the workgroup's current tile
@@ -1699,20 +1699,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
             load_g(1);
 #pragma unroll
             for (int j = 0; j < JC; ++j) {
-#ifdef SRCDSP_TUNE_HALF_LDS
-                // tuning probe only (wrong outputs): every other window
-                // granule is an opaque register value instead of an LDS read,
-                // so the tap loop issues the same VALU work with half the
-                // ds_read_b128 -- the price of the window reads
-                if ((j & 3) == 1 && ((j >> 2) & 1)) {
-                    const int c = -1 - (j >> 2);
-                    for (int k = 0; k < 4; ++k) asm volatile("" : "=v"(Dr[OFF + 4 * c + k]), "=v"(Di[OFF + 4 * c + k]));
-                } else if ((j & 3) == 1) {
-                    load_g(-1 - (j >> 2));
-                }
-#else
                 if ((j & 3) == 1) load_g(-1 - (j >> 2));
-#endif
                 if ((j & 15) == 0) asm volatile("" : "+s"(tp));
                 const uint32_t P = tp[j];
 #pragma unroll
