@@ -82,9 +82,19 @@ __device__ double crsqrt_u32(uint32_t n) {
 }
 
 // correlators.h:262-268 evaluated exactly
+// Fast path: with correctly rounded square roots, sqrt(c) > sqrt(e) * 2.7 in
+// double holds exactly when c > 7.29 e up to a relative ~1e-15 (the roundings
+// of the two square roots, of 2.7 and of the product), so outside a 1e-9
+// relative band around c = 7.29 e the sign of c - 7.29 e (one fma) decides;
+// inside it, the exact square roots do.  In noise about a third of all
+// outputs are local peaks with energy above 300^2 and reach this test; the
+// exact path for every one of them cost ~9 % of the fused scan's VALU work.
 __device__ __forceinline__ bool corr_hit(uint32_t c2, uint32_t c1, uint32_t c0, uint32_t e1) {
     if (!(c1 > c2 && c1 > c0)) return false;
     if (e1 <= 90000u) return false;  // sqrt(e) > 300 in double <=> e >= 90001
+    const double dc = (double)c1, d = __builtin_fma(-7.29, (double)e1, dc);
+    if (d > 1e-9 * dc) return true;
+    if (d < -1e-9 * dc) return false;
     const double cm = crsqrt_u32(c1), em = crsqrt_u32(e1);
     return cm > em * 2.7;
 }
@@ -160,6 +170,11 @@ __global__ __launch_bounds__(kCorrBlock) void corr_eval(const uint32_t *__restri
 // the oldest real sample).
 constexpr int kCR = 16;       // outputs per lane
 constexpr int kCBlock = 256;  // lanes per workgroup
+// corr_scan_s1 at 5 waves per SIMD (<= 96 VGPRs; its spills are in the
+// epilogue, not the tap loop): -1.4 % against 4 (profiles/tuning/r04_corr_ab.txt)
+#ifndef SRCDSP_CORR_MINW
+#define SRCDSP_CORR_MINW 5
+#endif
 constexpr unsigned kCorrDot2MaxTaps = 8192;  // LDS image <= 64 KB
 
 // corr_eval's arithmetic for windows too long to stage (N*S + 255 samples
@@ -317,7 +332,7 @@ __device__ __forceinline__ unsigned load_best(const unsigned *best) {
     return __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(kCBlock) void corr_scan_s1(const uint32_t *__restrict__ in, long n,
+__global__ __launch_bounds__(kCBlock, SRCDSP_CORR_MINW) void corr_scan_s1(const uint32_t *__restrict__ in, long n,
                                                          const uint32_t *__restrict__ hist,
                                                          const uint32_t *__restrict__ ptaps, int N, int NP, unsigned cs,
                                                          uint32_t c_prev0, uint32_t c_prev1, uint32_t e_prev0,
@@ -350,6 +365,27 @@ __global__ __launch_bounds__(kCBlock) void corr_scan_s1(const uint32_t *__restri
     for (int r = 0; r < kCR; ++r) ar[r] = ai[r] = 0;
     int32_t e0 = 0;
     const int lb = t * kCR;
+    // The window energy of each lane's first output from 16-sample chunk sums
+    // instead of one dot2(x, x) per tap beside the 32 correlation dot2: lane
+    // t's window (tile samples lb .. lb + NP - 1, lb = 16 t) is sample chunks
+    // t .. t + NP/16 - 1.  Wrap-around uint32 sums, so equal to the direct sum.
+    {
+        __shared__ uint32_t csum[kCBlock + kCorrDot2MaxTaps / 16];
+        const int NCk = NP / 16;
+        for (int g = t; g < kCBlock + NCk - 1; g += kCBlock) {
+            uint32_t sg = 0;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const short2_t a = __builtin_bit_cast(short2_t, xs[lw(16 * g + k)]);
+                sg += (uint32_t)__builtin_amdgcn_sdot2(a, a, 0, false);
+            }
+            csum[g] = sg;
+        }
+        __syncthreads();
+        uint32_t eu = 0;
+        for (int g = 0; g < NCk; ++g) eu += csum[t + g];
+        e0 = (int32_t)eu;
+    }
     uint32_t A[kCR + 15], B[kCR + 15];
 #pragma unroll
     for (int j = 0; j < kCR - 1; ++j) B[16 + j] = xs[lw(lb + j)];
@@ -372,8 +408,6 @@ __global__ __launch_bounds__(kCBlock) void corr_scan_s1(const uint32_t *__restri
 #pragma unroll
         for (int mm = 0; mm < 16; ++mm) {
             const uint32_t p0 = pw[2 * mm], p1 = pw[2 * mm + 1];
-            const short2_t x0 = __builtin_bit_cast(short2_t, word(mm));
-            e0 = __builtin_amdgcn_sdot2(x0, x0, e0, false);
 #pragma unroll
             for (int r = 0; r < kCR; ++r) {
                 const short2_t x = __builtin_bit_cast(short2_t, word(mm + r));
