@@ -81,6 +81,14 @@ __device__ double crsqrt_u32(uint32_t n) {
     return s;  // unreachable: the hardware estimate is within a few ulp
 }
 
+// the test's band case with correctly rounded square roots; out of line: the
+// scan tests 16 outputs per lane, and inlined 16 times this rarely taken path
+// made up 40 % of the kernel's code
+__device__ __attribute__((noinline)) bool corr_hit_exact(uint32_t c1, uint32_t e1) {
+    const double cm = crsqrt_u32(c1), em = crsqrt_u32(e1);
+    return cm > em * 2.7;
+}
+
 // correlators.h:262-268 evaluated exactly
 // Fast path: with correctly rounded square roots, sqrt(c) > sqrt(e) * 2.7 in
 // double holds exactly when c > 7.29 e up to a relative ~1e-15 (the roundings
@@ -95,8 +103,7 @@ __device__ __forceinline__ bool corr_hit(uint32_t c2, uint32_t c1, uint32_t c0, 
     const double dc = (double)c1, d = __builtin_fma(-7.29, (double)e1, dc);
     if (d > 1e-9 * dc) return true;
     if (d < -1e-9 * dc) return false;
-    const double cm = crsqrt_u32(c1), em = crsqrt_u32(e1);
-    return cm > em * 2.7;
+    return corr_hit_exact(c1, e1);
 }
 
 // ------------------------------------------------------------------ kernels
@@ -336,8 +343,7 @@ __global__ __launch_bounds__(kCBlock, SRCDSP_CORR_MINW) void corr_scan_s1(const 
                                                          const uint32_t *__restrict__ hist,
                                                          const uint32_t *__restrict__ ptaps, int N, int NP, unsigned cs,
                                                          uint32_t c_prev0, uint32_t c_prev1, uint32_t e_prev0,
-                                                         uint32_t *__restrict__ corr_out,
-                                                         uint32_t *__restrict__ en_out, unsigned *best) {
+                                                         unsigned *best) {
     extern __shared__ __attribute__((aligned(16))) uint32_t xs[];
     __shared__ uint32_t prev_c[kCBlock + 1][2], prev_e[kCBlock + 1];
     __shared__ unsigned dead_any, best0;
@@ -465,13 +471,19 @@ __global__ __launch_bounds__(kCBlock, SRCDSP_CORR_MINW) void corr_scan_s1(const 
             prev_e[0] = ex_e;
         }
     }
-    // this lane's correlation values and (sliding) energies
-    uint32_t cv[kCR], ev[kCR];
+    // this lane's correlation values and (sliding) energies, tested as they are
+    // formed: outputs 2..15 need only the lane's own values, so only outputs 0
+    // and 1 (which need the previous lane's last values) wait for the barrier,
+    // and three values per lane live across it instead of 32 (at 5 waves per
+    // SIMD the 32 spilled to scratch: 2.25 x the algorithmic HBM bytes)
     uint32_t e = (uint32_t)e0;  // the direct sum ran over NP window words, the first pad before the real window
     for (int q = 0; q < pad; ++q) {
         const short2_t a = __builtin_bit_cast(short2_t, xs[lw(lb + q)]);
         e -= (uint32_t)__builtin_amdgcn_sdot2(a, a, 0, false);
     }
+    uint32_t c_0 = 0, c_1 = 0, e_0 = 0;  // outputs 0 and 1, for the tests after the barrier
+    uint32_t cm2 = 0, cm1 = 0, em1 = 0;  // the two outputs before r, the energy before r
+    long hit = -1;                       // first hit among outputs 2..15
 #pragma unroll
     for (int r = 0; r < kCR; ++r) {
         if (r > 0) {  // E_i = E_{i-1} + |x_i|^2 - |x_{i-N}|^2
@@ -479,31 +491,30 @@ __global__ __launch_bounds__(kCBlock, SRCDSP_CORR_MINW) void corr_scan_s1(const 
             const short2_t a = __builtin_bit_cast(short2_t, xn), b = __builtin_bit_cast(short2_t, xo);
             e += (uint32_t)__builtin_amdgcn_sdot2(a, a, 0, false) - (uint32_t)__builtin_amdgcn_sdot2(b, b, 0, false);
         }
-        cv[r] = corr_value(ar[r], ai[r], cs);
-        ev[r] = e >> ((unsigned)((int)cs / 2) & 31u);
+        const uint32_t c = corr_value(ar[r], ai[r], cs), ev = e >> ((unsigned)((int)cs / 2) & 31u);
+        const long i = i0 + lb + r;
+        if (r == 0) {
+            c_0 = c;
+            e_0 = ev;
+        } else if (r == 1) {
+            c_1 = c;
+        } else if (!dead && hit < 0 && i < n && corr_hit(cm2, cm1, c, em1)) {
+            hit = i;
+        }
+        cm2 = cm1;
+        cm1 = c;
+        em1 = ev;
     }
-    prev_c[t + 1][0] = cv[kCR - 1];
-    prev_c[t + 1][1] = cv[kCR - 2];
-    prev_e[t + 1] = ev[kCR - 1];
+    prev_c[t + 1][0] = cm1;  // output 15
+    prev_c[t + 1][1] = cm2;  // output 14
+    prev_e[t + 1] = em1;
     if (dead) dead_any = 1;
     __syncthreads();
     if (dead_any) return;  // outputs past a known hit: nothing to record
-    const uint32_t cm1 = prev_c[t][0], cm2 = prev_c[t][1], em1 = prev_e[t];
-    long hit = -1;
-#pragma unroll
-    for (int r = 0; r < kCR; ++r) {
-        const long i = i0 + lb + r;
-        if (i < n) {
-            if (corr_out) {  // (the product passes none: corr_point recomputes what the registers need)
-                corr_out[i] = cv[r];
-                en_out[i] = ev[r];
-            }
-            const uint32_t c1 = r >= 1 ? cv[r - 1] : cm1;
-            const uint32_t c2 = r >= 2 ? cv[r - 2] : (r == 1 ? cm1 : cm2);
-            const uint32_t e1 = r >= 1 ? ev[r - 1] : em1;
-            if (hit < 0 && corr_hit(c2, c1, cv[r], e1)) hit = i;
-        }
-    }
+    const uint32_t pc1 = prev_c[t][0], pc2 = prev_c[t][1], pe1 = prev_e[t];
+    const long i = i0 + lb;
+    if (i + 1 < n && corr_hit(pc1, c_0, c_1, e_0)) hit = i + 1;
+    if (i < n && corr_hit(pc2, pc1, c_0, pe1)) hit = i;
     if (hit >= 0) atomicMin(best, (unsigned)hit);
 }
 
@@ -630,7 +641,7 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
         const long blocks = (n + TO - 1) / TO;
         const size_t smem = 4 * (size_t)(((TO + c.NP + 1) / kCR + 2) * (kCR + 4));
         hipLaunchKernelGGL(corr_scan_s1, dim3((unsigned)blocks), dim3(kCBlock), smem, s, d_in, n, hist, c.d_ptaps,
-                           (int)c.N, (int)c.NP, cs, c.corr[0], c.corr[1], c.energy[0], nullptr, nullptr, c.d_best);
+                           (int)c.N, (int)c.NP, cs, c.corr[0], c.corr[1], c.energy[0], c.d_best);
         SRCDSP_HIP_TRY(hipGetLastError());
         hipLaunchKernelGGL(corr_point, dim3(1), dim3(256), 0, s, d_in, n, hist, c.d_coef, c.N, c.S, cs,
                            (const unsigned *)c.d_best, c.d_best + 2);
