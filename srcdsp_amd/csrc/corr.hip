@@ -177,8 +177,8 @@ __global__ __launch_bounds__(kCorrBlock) void corr_eval(const uint32_t *__restri
 // the oldest real sample).
 constexpr int kCR = 16;       // outputs per lane
 constexpr int kCBlock = 256;  // lanes per workgroup
-// corr_scan_s1 at 5 waves per SIMD (<= 96 VGPRs; its spills are in the
-// epilogue, not the tap loop): -1.4 % against 4 (profiles/tuning/r04_corr_ab.txt)
+// corr_scan_s1 at 5 waves per SIMD (<= 96 VGPRs, no spills): -1.4 % against 4
+// (profiles/tuning/r04_corr_ab.txt)
 #ifndef SRCDSP_CORR_MINW
 #define SRCDSP_CORR_MINW 5
 #endif
@@ -353,15 +353,34 @@ __global__ __launch_bounds__(kCBlock, SRCDSP_CORR_MINW) void corr_scan_s1(const 
     __syncthreads();
     if ((long)best0 < i0) return;  // a hit before this tile is already known (block-uniform)
     // taps front-padded with NP - N zero taps (NP = 16 ceil(N/16), as corr_eval_dot2)
-    const long base = i0 - (NP - 1);
-    const int span = TO + NP - 1;
     const int pad = NP - N;
+    // tile sample l (input word i0 - (NP - 1) + l, l = 0 .. TO + NP - 2) -> LDS word lw(l)
     auto lw = [&](int l) { int lp = l + 1; return lp + 4 * (lp / kCR); };
-    for (int l = threadIdx.x; l < span; l += kCBlock) {
-        long j = base + l;
-        uint32_t w = 0;
-        if (j < n) w = j >= 0 ? in[j] : (j + (N - 1) >= 0 ? hist[j + (N - 1)] : 0u);
-        xs[lw(l)] = w;
+    // Staging by 16-B granules: LDS chunk c (20 words, the last 4 padding)
+    // holds tile samples 16c - 1 .. 16c + 14, i.e. input words j0 + 16c + 4q +
+    // (0..3), j0 = i0 - NP: 16-aligned, so an aligned input is read with one
+    // dwordx4 per granule; granules that reach before sample 0 or past n, and
+    // misaligned inputs, go word by word (history before 0, zeros past n).
+    const int NC = (TO + NP) / kCR;  // chunks: tile samples -1 .. TO + NP - 2
+    const long j0 = i0 - NP;
+    const bool al16 = ((uintptr_t)in & 15u) == 0;
+    uint4 *xs4 = (uint4 *)xs;
+    for (int gq = threadIdx.x; gq < 4 * NC; gq += kCBlock) {
+        const int c = gq >> 2, q = gq & 3;
+        const long j = j0 + 16L * c + 4 * q;
+        uint4 v;
+        if (al16 && j >= 0 && j + 4 <= n) {
+            v = *(const uint4 *)(in + j);
+        } else {
+            uint32_t w[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const long jk = j + k;
+                w[k] = jk < n ? (jk >= 0 ? in[jk] : (jk + (N - 1) >= 0 ? hist[jk + (N - 1)] : 0u)) : 0u;
+            }
+            v = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        xs4[5 * c + q] = v;
     }
     if (threadIdx.x == 0) dead_any = 0;
     __syncthreads();
@@ -372,23 +391,30 @@ __global__ __launch_bounds__(kCBlock, SRCDSP_CORR_MINW) void corr_scan_s1(const 
     int32_t e0 = 0;
     const int lb = t * kCR;
     // The window energy of each lane's first output from 16-sample chunk sums
-    // instead of one dot2(x, x) per tap beside the 32 correlation dot2: lane
-    // t's window (tile samples lb .. lb + NP - 1, lb = 16 t) is sample chunks
-    // t .. t + NP/16 - 1.  Wrap-around uint32 sums, so equal to the direct sum.
+    // instead of one dot2(x, x) per tap beside the 32 correlation dot2.  Lane
+    // t's window is tile samples lb .. lb + NP - 1 (lb = 16 t); LDS chunks
+    // t .. t + NP/16 - 1 hold samples lb - 1 .. lb + NP - 2, so the sum of their
+    // chunk sums, less |x[lb - 1]|^2, plus |x[lb + NP - 1]|^2 (word 0 of chunk
+    // t + NP/16).  A chunk sum reads its chunk as 4 ds_read_b128 (conflict-free
+    // at the 80-B chunk stride).  Wrap-around uint32 sums: equal to the direct sum.
     {
         __shared__ uint32_t csum[kCBlock + kCorrDot2MaxTaps / 16];
         const int NCk = NP / 16;
+        auto sq = [](uint32_t w) {
+            const short2_t a = __builtin_bit_cast(short2_t, w);
+            return (uint32_t)__builtin_amdgcn_sdot2(a, a, 0, false);
+        };
         for (int g = t; g < kCBlock + NCk - 1; g += kCBlock) {
             uint32_t sg = 0;
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const short2_t a = __builtin_bit_cast(short2_t, xs[lw(16 * g + k)]);
-                sg += (uint32_t)__builtin_amdgcn_sdot2(a, a, 0, false);
+            for (int q = 0; q < 4; ++q) {
+                const uint4 v = xs4[5 * g + q];
+                sg += sq(v.x) + sq(v.y) + sq(v.z) + sq(v.w);
             }
             csum[g] = sg;
         }
         __syncthreads();
-        uint32_t eu = 0;
+        uint32_t eu = sq(xs[20 * (t + NCk)]) - sq(xs[20 * t]);
         for (int g = 0; g < NCk; ++g) eu += csum[t + g];
         e0 = (int32_t)eu;
     }
