@@ -5,12 +5,13 @@ Default workload = BASELINE.json configs[1] (the headline metric): the 127-tap
 complex<float> decimate-by-4 FilterDnsamplingFir over 2^28 device-resident
 synthetic samples, one step() per timed step (one kernel launch), FMA float
 contract.  With --gpus N (launched by torch.distributed.run) every rank owns
-8 channels of 2^28 samples (configs[2]'s layout: 64 channels over 8 GPUs at
-N = 8, one batched launch per step per rank; --channels-per-gpu overrides):
-weak scaling, no collective in the timed region; the RCCL gather of every
-channel's decimated output to rank 0 (32 GiB at N = 8) is timed separately
-(gather_ms).  N = 1 stays configs[1] (one channel), so SCALE's N = 1 value is
-BENCH's.
+the same work as N = 1 -- one 2^28-sample channel of its own -- so the N = 1,
+2, 4, 8 values form one weak-scaling series (no collective in the timed
+region).  Beside it, in the same line, `configs2_share` measures configs[2]'s
+layout: 8 channels of 2^28 per GPU (64 over 8 GPUs), one batched step per
+rank, at every N (so that series is weak scaling too), and the RCCL gather of
+every channel's decimated output to rank 0 (32 GiB at N = 8), timed apart.
+--channels-per-gpu C makes C channels per GPU the main series instead.
 
 Other workloads (--workload): mixdecim (config 4, mixer -> fixed-point
 decimator, fused), corr (config 5, 1024-lag correlator), fir (config 1 shape on
@@ -53,9 +54,11 @@ def parse():
     p.add_argument("--workload", default="decim", choices=["decim", "mixdecim", "ci16decim", "corr", "fir", "up", "fifo", "iq"])
     p.add_argument("--samples", type=int, default=None,
                    help="input samples per channel per step (default 2^28; corr: 2^26, config 5's 64 Msamp)")
-    # default (decim): 1 channel at N = 1 (configs[1]), 8 per GPU at N > 1
-    # (configs[2]: 64 channels at N = 8); see channel_layout()
+    # default (decim): one 2^28 channel per GPU at every N (configs[1]'s work
+    # per GPU), plus the configs[2] per-GPU share (8 channels) beside it; see
+    # channel_layout() and share_layout()
     p.add_argument("--channels-per-gpu", type=int, default=None)
+    p.add_argument("--no-share", action="store_true", help="skip the configs[2] per-GPU share measurement")
     p.add_argument("--fp", default="fma", choices=["fma", "strict"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=1 << 27, help="samples timed on the reference CPU path")
@@ -93,13 +96,29 @@ def spawn_ranks(args) -> int | None:
     return subprocess.run(cmd).returncode
 
 
+CONFIG2_CHANNELS, CONFIG2_PER_GPU = 64, 8  # BASELINE configs[2]: 64 channels, 8 per GPU at N = 8
+
+
+def layout_label(cpg: int, world: int) -> str:
+    """Which BASELINE config a decim layout is: configs[1] is one 2^28
+    channel on one GPU, configs[2] is 64 channels, 8 per GPU on 8 GPUs; the
+    same per-GPU layouts at other N say so instead of claiming the config."""
+    if cpg == 1:
+        return "configs[1]" if world == 1 else f"configs[1] on each of {world} GPUs ({world} independent channels)"
+    if cpg == CONFIG2_PER_GPU:
+        total = cpg * world
+        return "configs[2]" if total == CONFIG2_CHANNELS else \
+            f"configs[2] per-GPU layout ({total} of {CONFIG2_CHANNELS} channels)"
+    return "custom"
+
+
 def channel_layout(args, world: int, L: int | None = None) -> dict:
-    """Channel layout of the decim workload (BASELINE configs[1] / configs[2]).
-    N = 1: one 2^28-sample channel (configs[1], the headline).  N > 1: 8
-    channels per GPU, block-partitioned (srcdsp_amd.dist.channels_for_rank),
-    so N = 8 holds configs[2]'s 64 independent 256 Msamp channels; the gather
-    moves every channel's decimated output (L/4 complex<float>) to rank 0.
-    Other workloads run one buffer per rank."""
+    """Channel layout of the main series (decim workload): one 2^28-sample
+    channel per GPU at every N unless --channels-per-gpu says otherwise, so
+    the per-GPU work is the same at N = 1, 2, 4, 8 (weak scaling).  Channels
+    are block-partitioned (srcdsp_amd.dist.channels_for_rank).  Other
+    workloads run one buffer per rank.  The main series has no collective;
+    the gather belongs to the configs[2] share (share_layout)."""
     if L is None:
         L = args.samples if args.samples is not None else (1 << 28)
         L -= L % 4
@@ -108,10 +127,26 @@ def channel_layout(args, world: int, L: int | None = None) -> dict:
     elif args.channels_per_gpu is not None:
         cpg = args.channels_per_gpu
     else:
-        cpg = 1 if world == 1 else 8
+        cpg = 1
     total = cpg * world
     return {"channels_per_gpu": cpg, "channels_total": total, "samples_per_channel": L,
-            "gather_bytes": total * (L // 4) * 8 if args.workload == "decim" and world > 1 else 0}
+            "baseline_config": layout_label(cpg, world) if args.workload == "decim" else None}
+
+
+def share_layout(args, world: int, L: int | None = None) -> dict | None:
+    """configs[2]'s per-GPU share measured beside the main series: 8 channels
+    of 2^28 per GPU at every N (64 in all at N = 8), and the gather of every
+    channel's decimated output to rank 0.  None when not measured (other
+    workloads, an explicit --channels-per-gpu, --no-share)."""
+    if args.workload != "decim" or args.channels_per_gpu is not None or getattr(args, "no_share", False):
+        return None
+    if L is None:
+        L = args.samples if args.samples is not None else (1 << 28)
+        L -= L % 4
+    total = CONFIG2_PER_GPU * world
+    return {"channels_per_gpu": CONFIG2_PER_GPU, "channels_total": total, "samples_per_channel": L,
+            "baseline_config": layout_label(CONFIG2_PER_GPU, world),
+            "gather_bytes": total * (L // 4) * 8 if world > 1 else 0}
 
 
 def dry_run(args) -> None:
@@ -133,7 +168,8 @@ def dry_run(args) -> None:
     sys.stdout.flush()
     os.write(1, (json.dumps({"dry_run": True, "rank": rank, "world": world, "world_seen": seen,
                              "gpus": args.gpus, "workload": args.workload,
-                             "layout": channel_layout(args, world)}) + "\n").encode())
+                             "layout": channel_layout(args, world),
+                             "share_layout": share_layout(args, world)}) + "\n").encode())
     if world != args.gpus or seen != args.gpus:
         raise SystemExit(f"bench: rank {rank} sees world {world}/{seen}, --gpus {args.gpus}")
 
@@ -656,6 +692,65 @@ def pmc_traffic(args, work_name, per_launch_samples):
     return e.get("hbm_bytes_per_launch"), "rocprofv3 PMC, " + e.get("correction", "")
 
 
+# ---------------------------------------------------------------- timing
+def timed_steps(work, args, world, torch):
+    """W untimed warm-up steps, then K timed steps bracketed by barrier +
+    synchronize on both sides.  Returns (max-over-ranks wall seconds, the HIP
+    event duration of every timed step in ms, on the launch stream)."""
+    from srcdsp_amd.dist import max_over_ranks
+    stream = torch.cuda.current_stream()
+    for _ in range(args.warmup):
+        work.step()
+    barrier(world)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    barrier(world)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        work.step()
+        ev[i][1].record(stream)
+    barrier(world)
+    t1 = time.perf_counter()
+    wall = max_over_ranks(t1 - t0, world, device=COLL_DEV)
+    return wall, [a.elapsed_time(b) for a, b in ev]
+
+
+def measure_share(S, torch, args, world, rank, L, slay) -> dict:
+    """configs[2]'s per-GPU share beside the main series: 8 channels of 2^28
+    per GPU, one batched step per rank, same warm-up/steps protocol (it runs
+    right after the main series, on a warm chip); then the RCCL gather of every
+    rank's decimated channels to rank 0, timed apart (never part of a value)."""
+    from srcdsp_amd.dist import gather_to_root
+    work = DecimWorkload(S, torch, L, slay["channels_per_gpu"], rank, args.fp)
+    wall, kern_ms = timed_steps(work, args, world, torch)
+    kern_avg_ms = float(np.mean(kern_ms))
+    per_launch = L * slay["channels_per_gpu"]
+    achieved = work.bytes_per_sample * per_launch / (kern_avg_ms * 1e-3) / 1e9
+    out = {"baseline_config": slay["baseline_config"], "channels_per_gpu": slay["channels_per_gpu"],
+           "channels_total": slay["channels_total"], "samples_per_channel": L,
+           "value": round(per_launch * world * args.steps / wall / 1e6, 2), "unit": "Msamples/s",
+           "ms_per_step": round(wall / args.steps * 1e3, 4), "scaling": "weak",
+           "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 4), "per_gpu": True,
+                        "channels_per_launch": slay["channels_per_gpu"], "kernel_ms": round(kern_avg_ms, 4),
+                        "algorithmic_bytes_per_launch": int(work.bytes_per_sample * per_launch)},
+           "timed": "after the main series (warm chip); batched step over the rank's 8 channels"}
+    if world > 1 and not args.no_gather:
+        barrier(world)
+        g0 = time.perf_counter()
+        bufs = gather_to_root(work.y if COLL_DEV else work.y.cpu(), world, rank)
+        barrier(world)
+        gather_ms = (time.perf_counter() - g0) * 1e3
+        del bufs
+        nbytes = int(world * work.y.numel() * work.y.element_size())
+        assert nbytes == slay["gather_bytes"]
+        out.update(gather_ms=round(gather_ms, 3), gather_bytes=nbytes,
+                   gather_gbs=round(nbytes / (gather_ms * 1e-3) / 1e9, 1))
+    del work
+    torch.cuda.empty_cache()
+    return out
+
+
 # ---------------------------------------------------------------- main
 def main():
     args = parse()
@@ -675,32 +770,16 @@ def main():
         raise SystemExit(f"bench: --gpus {args.gpus} but the launcher started {world} rank(s) "
                          f"(process group: {reported})")
     import srcdsp_amd as S
-    from srcdsp_amd.dist import gather_to_root, max_over_ranks
     S.lib()  # loud failure if the HIP library is missing
     if args.samples is None:
         args.samples = (1 << 26) if args.workload == "corr" else (1 << 28)
     L = args.samples - args.samples % 4
     lay = channel_layout(args, world, L)
+    slay = share_layout(args, world, L)  # before channels_per_gpu is filled in
     args.channels_per_gpu = lay["channels_per_gpu"]
     work = WORKLOADS[args.workload](S, torch, L, args.channels_per_gpu, rank, args.fp)
-    stream = torch.cuda.current_stream()
-
-    for _ in range(args.warmup):
-        work.step()
-    barrier(world)
-
-    # timed region: K steps, barrier + synchronize on both sides
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    barrier(world)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        work.step()
-        ev[i][1].record(stream)
-    barrier(world)
-    t1 = time.perf_counter()
-    wall = max_over_ranks(t1 - t0, world, device=COLL_DEV)
-    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    work_name, work_dtype = work.name, work.dtype
+    wall, kern_ms = timed_steps(work, args, world, torch)
     kern_avg_ms = float(np.mean(kern_ms))
     if args.dump_steps and rank == 0:
         print("step_ms " + " ".join(f"{v:.4f}" for v in kern_ms), file=sys.stderr, flush=True)
@@ -717,16 +796,6 @@ def main():
         total_samples = ((idx + 2) if found else L) * args.steps
     value = total_samples / wall / 1e6
     ms_per_step = wall / args.steps * 1e3
-
-    gather_ms = None
-    if world > 1 and not args.no_gather and args.workload == "decim":
-        # configs[2]: gather every rank's decimated channels to rank 0 over RCCL (xGMI)
-        barrier(world)
-        g0 = time.perf_counter()
-        bufs = gather_to_root(work.y if COLL_DEV else work.y.cpu(), world, rank)
-        barrier(world)
-        gather_ms = (time.perf_counter() - g0) * 1e3
-        del bufs
 
     per_launch_samples = L * args.channels_per_gpu if args.workload == "decim" else L
     if args.workload in ("up", "fifo", "iq"):
@@ -781,12 +850,16 @@ def main():
                 "kernel": work.name, "kernel_ms": round(kern_avg_ms, 4), "scanned_samples": int(scanned),
                 "hbm_gbs_for_reference": round(achieved, 1)}
 
+    share = None
+    if slay is not None:
+        del work
+        torch.cuda.empty_cache()
+        share = measure_share(S, torch, args, world, rank, L, slay)
+
     if rank == 0:
-        cfg = {"workload": work.name, "samples_per_channel": L, "channels_per_gpu": args.channels_per_gpu,
+        cfg = {"workload": work_name, "samples_per_channel": L, "channels_per_gpu": args.channels_per_gpu,
                "channels_total": lay["channels_total"],
-               "baseline_config": ("configs[1]" if world == 1 and lay["channels_total"] == 1 else
-                                   "configs[2]" if lay["channels_per_gpu"] == 8 else "custom")
-               if args.workload == "decim" else None,
+               "baseline_config": lay["baseline_config"],
                "taps": {"decim": 127, "mixdecim": 127, "ci16decim": 127, "fir": 31, "up": 128}.get(args.workload),
                "decimation": {"decim": 4, "mixdecim": 4, "ci16decim": 4}.get(args.workload), "interpolation": 4 if args.workload == "up" else None,
                "fp_contract": args.fp,
@@ -797,27 +870,18 @@ def main():
             cfg.update({"samples_per_channel": work.n, "taps": 127, "decimation": 4,
                         "timed": ("host block -> pinned staging -> H2D -> HBM (FIFO ring or capture) -> "
                                   "mixer->decimator chain, one block per step; PCIe included")})
-        line = {"metric": METRIC if args.workload == "decim" else f"Msamples/sec (in), {work.name}",
+        line = {"metric": METRIC if args.workload == "decim" else f"Msamples/sec (in), {work_name}",
                 "value": round(value, 2), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
                 "scaling": "strong" if args.workload == "corr" and world > 1 else "weak",
-                "vs_baseline": None, "dtype": work.dtype,
+                "vs_baseline": None, "dtype": work_dtype,
                 "data": "synthetic (counter-based splitmix64 integer samples, SURVEY §8d)", "config": cfg,
                 "roofline": roof, "hbm_read": hbm_read, "world_size_reported": reported,
                 "backend": BACKEND if world > 1 else None}
         if args.workload == "decim":
-            # `roofline` is rank 0's own batched launch (its channels_per_gpu
-            # channels), i.e. per GPU; at N > 1 one launch covers 8 channels and
-            # the clock holds steady across it, whereas the N = 1 line times one
-            # 2^28 channel per launch inside the post-idle clock transient
-            # (DESIGN §5.1), so the per-GPU fraction differs between the two
+            # `roofline` is rank 0's own launch(es): per GPU, the same work at every N
             roof["per_gpu"] = True
             roof["channels_per_launch"] = args.channels_per_gpu
-        if gather_ms is not None:
-            line["gather_ms"] = round(gather_ms, 3)
-            line["gather_bytes"] = int(world * work.y.numel() * work.y.element_size())
-            assert line["gather_bytes"] == lay["gather_bytes"]
-            line["gather_gbs"] = round(line["gather_bytes"] / (gather_ms * 1e-3) / 1e9, 1)
         if args.workload == "corr":
             line["detection"] = list(work.last)
         if not args.no_cpu_baseline and world == 1:
@@ -829,7 +893,7 @@ def main():
         if args.workload == "decim" and world == 1 and not args.no_pcie:
             line["pcie_inclusive"] = pcie_inclusive(S)
         print(json.dumps(line), flush=True)
-    if hasattr(work, "close"):
+    if slay is None and hasattr(work, "close"):
         work.close()
     if world > 1:
         import torch.distributed as dist

@@ -16,6 +16,16 @@
  *
  * Results are those of C separate FilterDnsamplingFir objects, bit for bit.
  *
+ * Ordering: step() and gather() run on the comm streams, which are
+ * non-blocking -- they wait neither for the null stream nor for the caller's
+ * streams, and the caller's streams do not wait for them.  Caller work that
+ * fills d_in or reads d_out / d_root must run on comm.stream(r), or after
+ * comm.synchronize(), or be ordered with
+ *   comm.waitFor(r, s);  // comm stream r waits for what `s` queued so far
+ *   comm.signal(r, s);   // `s` waits for what comm stream r queued so far
+ *   e.g. fill d_in[r] on s; comm.waitFor(r, s); f.step(...); f.gather(...);
+ *        comm.signal(root, s); copy d_root out on s; hipStreamSynchronize(s);
+ *
  * Lifetime: a ShardedDnsamplingFir holds its own reference to the
  * communicator (srcdsp_decim_sharded_create), so the GpuComm may be destroyed
  * before the operators built on it.
@@ -53,6 +63,15 @@ public:
         return s;
     }
     void synchronize() { srcdsp_detail::check(srcdsp_comm_synchronize(c_), "GpuComm::synchronize"); }
+    /// work queued later on rank's comm stream waits for everything queued on
+    /// `stream` (a hipStream_t on rank's device, as void*) so far
+    void waitFor(int rank, void *stream) {
+        srcdsp_detail::check(srcdsp_comm_wait_stream(c_, rank, stream), "GpuComm::waitFor");
+    }
+    /// work queued later on `stream` waits for everything queued on rank's comm stream so far
+    void signal(int rank, void *stream) {
+        srcdsp_detail::check(srcdsp_comm_signal_stream(c_, rank, stream), "GpuComm::signal");
+    }
     srcdsp_comm_t handle() const { return c_; }
 
 private:

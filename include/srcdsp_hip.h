@@ -299,6 +299,18 @@ SRCDSP_API int srcdsp_comm_info(srcdsp_comm_t c, int *ndev, int *devs);
 SRCDSP_API int srcdsp_comm_stream(srcdsp_comm_t c, int rank, void **stream);
 /* wait for every rank's stream */
 SRCDSP_API int srcdsp_comm_synchronize(srcdsp_comm_t c);
+/* ORDERING RULE.  The comm streams are non-blocking: they do not wait for the
+ * null stream or for any stream of the caller, and the caller's streams do
+ * not wait for them.  Caller work that writes a rank's d_in, or touches its
+ * d_out / the gather target d_root, must run on comm stream(rank), or after
+ * srcdsp_comm_synchronize, or be ordered by these two calls (no host block):
+ *   srcdsp_comm_wait_stream(c, r, s):   work queued later on rank r's comm
+ *       stream (steps, gathers) waits for everything queued on `s` so far;
+ *   srcdsp_comm_signal_stream(c, r, s): work queued later on `s` waits for
+ *       everything queued on rank r's comm stream so far.
+ * `s` is a hipStream_t (as void*) on rank r's device; NULL = its null stream. */
+SRCDSP_API int srcdsp_comm_wait_stream(srcdsp_comm_t c, int rank, void *stream);
+SRCDSP_API int srcdsp_comm_signal_stream(srcdsp_comm_t c, int rank, void *stream);
 
 /* `channels` independent FilterDnsamplingFir objects of one configuration
  * (same variant/M/taps/flags as srcdsp_decim_create), block-partitioned over
@@ -318,7 +330,7 @@ SRCDSP_API int srcdsp_decim_sharded_channel(srcdsp_decim_sharded_t h, int ch, sr
 /* one step() of every channel: d_in[r] / d_out[r] are device pointers on
  * rank r's device holding its count_r channels as rows in_stride / out_stride
  * samples apart; n_in samples per channel (n_in % M == 0).  Asynchronous on
- * the comm streams. */
+ * the comm streams (ORDERING RULE above). */
 SRCDSP_API int srcdsp_decim_sharded_step(srcdsp_decim_sharded_t h, const void *const *d_in, size_t in_stride,
                                          void *const *d_out, size_t out_stride, size_t n_in);
 /* reset every channel (dnsampling_filters.h:56-60), each on its own device */
@@ -334,7 +346,7 @@ SRCDSP_API int srcdsp_decim_sharded_step_host(srcdsp_decim_sharded_t h, const vo
  * channels*n_out samples).  ncclGather (rccl.h:745) when every rank holds the
  * same number of contiguous rows, else grouped ncclSend/ncclRecv
  * (rccl.h:700,720) with the root's own rows copied on its device.
- * Asynchronous on the comm streams. */
+ * Asynchronous on the comm streams (ORDERING RULE above). */
 SRCDSP_API int srcdsp_decim_sharded_gather(srcdsp_decim_sharded_t h, void *const *d_out, size_t out_stride,
                                            size_t n_out, void *d_root, int root);
 

@@ -91,6 +91,8 @@ SIGNATURES = {
     "srcdsp_comm_info": (I, [VP, IP, IP]),
     "srcdsp_comm_stream": (I, [VP, I, HP]),
     "srcdsp_comm_synchronize": (I, [VP]),
+    "srcdsp_comm_wait_stream": (I, [VP, I, VP]),
+    "srcdsp_comm_signal_stream": (I, [VP, I, VP]),
     "srcdsp_decim_sharded_create": (I, [HP, VP, I, I, U, VP, I, U]),
     "srcdsp_decim_sharded_destroy": (I, [VP]),
     "srcdsp_decim_sharded_partition": (I, [VP, I, IP, IP]),

@@ -131,6 +131,61 @@ def build(verbose: bool = False, jobs: int = 8, defines: tuple[str, ...] = (), l
     return LIB
 
 
+TEST_BUILD = os.path.join(ROOT, "tests", "_build")
+CORR_HIT_PROBE = os.path.join(TEST_BUILD, "libcorr_hit_probe.so")
+# Test-only variants of the library: the product's objects with ONE translation
+# unit recompiled under a test define.  Never loaded by the package.
+#   corr_exact: the correlator's detection test always on the correctly rounded
+#     square roots (corr_hit.h), so the suite can require identical detections
+#     with and without the fast sign test;
+#   shared_dev: multi.hip honouring SRCDSP_COMM_SHARED_DEVICES=1, so the
+#     multi-device C ABI can be rehearsed at ndev > 1 on one GPU through the
+#     test-only communicator library (tests/rccl_stub); named libsrcdsp_hip.so in
+#     its own directory so the C++ test program links it as -lsrcdsp_hip.
+TEST_VARIANTS = {
+    "corr_exact": ("corr.hip", "SRCDSP_CORR_ALWAYS_EXACT", os.path.join(TEST_BUILD, "libsrcdsp_hip_corr_exact.so")),
+    "shared_dev": ("multi.hip", "SRCDSP_TEST_SHARED_DEVICES", os.path.join(TEST_BUILD, "shared_dev", "libsrcdsp_hip.so")),
+}
+CORR_EXACT_LIB = TEST_VARIANTS["corr_exact"][2]
+SHARED_DEV_LIB = TEST_VARIANTS["shared_dev"][2]
+
+
+def build_test_probes(verbose: bool = False) -> list[str]:
+    """Test-only artefacts (tests/_build/, git-ignored, travel to the GPU box
+    like the library): the corr_hit probe kernel and the TEST_VARIANTS builds."""
+    build(verbose=verbose)
+    os.makedirs(TEST_BUILD, exist_ok=True)
+    hipcc = _hipcc()
+    hdrs = _headers()
+
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed:\n{r.stderr[-6000:]}")
+
+    probe_src = os.path.join(ROOT, "tests", "hip", "corr_hit_probe.hip")
+    if _stale(CORR_HIT_PROBE, [probe_src] + hdrs):
+        run([hipcc, *CXXFLAGS, "-shared", probe_src, "-o", CORR_HIT_PROBE])
+    out = [CORR_HIT_PROBE]
+    for name, (tu, define, lib) in TEST_VARIANTS.items():
+        obj_dir = OBJ + "_test_" + name
+        os.makedirs(obj_dir, exist_ok=True)
+        os.makedirs(os.path.dirname(lib), exist_ok=True)
+        src = os.path.join(CSRC, tu)
+        obj = os.path.join(obj_dir, tu + ".o")
+        if _stale(obj, [src] + hdrs):
+            run([hipcc, *CXXFLAGS, f"-D{define}", "-c", src, "-o", obj])
+        objs = [obj if os.path.basename(s) == tu else os.path.join(OBJ, os.path.basename(s) + ".o")
+                for s in sorted(glob.glob(os.path.join(CSRC, "*.hip")))]
+        if _stale(lib, objs):
+            run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs, "-ldl",
+                 f"-Wl,-rpath,{ROCM_LIB}"])
+        out.append(lib)
+    return out
+
+
 if __name__ == "__main__":
     # python -m srcdsp_amd.build [NAME DEFINE...]: with arguments, a tuning
     # build scripts/tune/ab/libsrcdsp_hip_NAME.so compiled with -DDEFINE...

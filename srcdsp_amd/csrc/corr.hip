@@ -21,6 +21,7 @@
 
 #include "ops.h"
 #include "decim_kernels.h"
+#include "corr_hit.h"
 
 namespace srcdsp {
 
@@ -49,62 +50,7 @@ struct srcdsp_corr_state {
     HostStage stage;
 };
 
-// ------------------------------------------------ exact double sqrt of uint32
-__device__ __forceinline__ bool rn_sqrt_ok(double s, uint32_t n) {
-    // s = m * 2^q is RN(sqrt(n)) iff (2m-1)^2 < n * 2^(2-2q) < (2m+1)^2 (no ties
-    // for integer n), checked in exact 128-bit integer arithmetic.
-    if (s <= 0) return n == 0 && s == 0;
-    unsigned long long b = (unsigned long long)__double_as_longlong(s);
-    int E = (int)((b >> 52) & 0x7ff);
-    unsigned long long m = (b & ((1ull << 52) - 1)) | (1ull << 52);
-    int K = -2 * (E - 1075) + 2;  // n * 2^K
-    if (K < 0 || K > 127 - 32) return false;
-    unsigned __int128 T = (unsigned __int128)n << K;
-    unsigned __int128 lo = (unsigned __int128)(2 * m - 1) * (2 * m - 1);
-    unsigned __int128 hi = (unsigned __int128)(2 * m + 1) * (2 * m + 1);
-    return lo < T && T < hi;
-}
-
-// neighbouring doubles of a positive finite value
-__device__ __forceinline__ double dnext(double s, long long d) {
-    return __longlong_as_double(__double_as_longlong(s) + d);
-}
-
-__device__ double crsqrt_u32(uint32_t n) {
-    if (n == 0) return 0.0;
-    const double s = __builtin_sqrt((double)n);
-    if (rn_sqrt_ok(s, n)) return s;
-    for (long long d = 1; d <= 4; ++d) {
-        if (rn_sqrt_ok(dnext(s, -d), n)) return dnext(s, -d);
-        if (rn_sqrt_ok(dnext(s, d), n)) return dnext(s, d);
-    }
-    return s;  // unreachable: the hardware estimate is within a few ulp
-}
-
-// the test's band case with correctly rounded square roots; out of line: the
-// scan tests 16 outputs per lane, and inlined 16 times this rarely taken path
-// made up 40 % of the kernel's code
-__device__ __attribute__((noinline)) bool corr_hit_exact(uint32_t c1, uint32_t e1) {
-    const double cm = crsqrt_u32(c1), em = crsqrt_u32(e1);
-    return cm > em * 2.7;
-}
-
-// correlators.h:262-268 evaluated exactly
-// Fast path: with correctly rounded square roots, sqrt(c) > sqrt(e) * 2.7 in
-// double holds exactly when c > 7.29 e up to a relative ~1e-15 (the roundings
-// of the two square roots, of 2.7 and of the product), so outside a 1e-9
-// relative band around c = 7.29 e the sign of c - 7.29 e (one fma) decides;
-// inside it, the exact square roots do.  In noise about a third of all
-// outputs are local peaks with energy above 300^2 and reach this test; the
-// exact path for every one of them cost ~9 % of the fused scan's VALU work.
-__device__ __forceinline__ bool corr_hit(uint32_t c2, uint32_t c1, uint32_t c0, uint32_t e1) {
-    if (!(c1 > c2 && c1 > c0)) return false;
-    if (e1 <= 90000u) return false;  // sqrt(e) > 300 in double <=> e >= 90001
-    const double dc = (double)c1, d = __builtin_fma(-7.29, (double)e1, dc);
-    if (d > 1e-9 * dc) return true;
-    if (d < -1e-9 * dc) return false;
-    return corr_hit_exact(c1, e1);
-}
+// the detection test (correlators.h:262-268): corr_hit / corr_hit_exact in corr_hit.h
 
 // ------------------------------------------------------------------ kernels
 __device__ __forceinline__ uint32_t corr_fetch(const uint32_t *in, const uint32_t *hist, long j, long NSm1) {
@@ -182,7 +128,13 @@ constexpr int kCBlock = 256;  // lanes per workgroup
 #ifndef SRCDSP_CORR_MINW
 #define SRCDSP_CORR_MINW 5
 #endif
-constexpr unsigned kCorrDot2MaxTaps = 8192;  // LDS image <= 64 KB
+// Dynamic LDS of the dot2 tiles: the staged window, corr_lds_words(NP) words
+// (chunks of 16 samples + 4 pad words); corr_scan_s1 appends its chunk sums,
+// kCBlock + NP/16 words.  At the largest NP, 8192: 61.6 KB + 3.0 KB (gfx950
+// gives a workgroup up to 160 KB).
+constexpr unsigned kCorrDot2MaxTaps = 8192;
+__host__ __device__ constexpr int corr_lds_words(int NP) { return ((kCBlock * kCR + NP + 1) / kCR + 2) * (kCR + 4); }
+__host__ __device__ constexpr int corr_scan_lds_words(int NP) { return corr_lds_words(NP) + kCBlock + NP / 16; }
 
 // corr_eval's arithmetic for windows too long to stage (N*S + 255 samples
 // past kCorrEvalMaxSmem of LDS, e.g. S in the thousands): one output per lane,
@@ -398,7 +350,7 @@ __global__ __launch_bounds__(kCBlock, SRCDSP_CORR_MINW) void corr_scan_s1(const 
     // t + NP/16).  A chunk sum reads its chunk as 4 ds_read_b128 (conflict-free
     // at the 80-B chunk stride).  Wrap-around uint32 sums: equal to the direct sum.
     {
-        __shared__ uint32_t csum[kCBlock + kCorrDot2MaxTaps / 16];
+        uint32_t *csum = xs + corr_lds_words(NP);  // kCBlock + NP/16 words (dynamic, sized by the host)
         const int NCk = NP / 16;
         auto sq = [](uint32_t w) {
             const short2_t a = __builtin_bit_cast(short2_t, w);
@@ -665,7 +617,7 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
     if (fused) {  // one launch, detection fused, in-flight early exit
         constexpr long TO = (long)kCBlock * kCR;
         const long blocks = (n + TO - 1) / TO;
-        const size_t smem = 4 * (size_t)(((TO + c.NP + 1) / kCR + 2) * (kCR + 4));
+        const size_t smem = 4 * (size_t)corr_scan_lds_words((int)c.NP);
         hipLaunchKernelGGL(corr_scan_s1, dim3((unsigned)blocks), dim3(kCBlock), smem, s, d_in, n, hist, c.d_ptaps,
                            (int)c.N, (int)c.NP, cs, c.corr[0], c.corr[1], c.energy[0], c.d_best);
         SRCDSP_HIP_TRY(hipGetLastError());
@@ -681,7 +633,7 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
             constexpr long TO = (long)kCBlock * kCR;
             const long per_phase = (se - sb + c.S - 1) / c.S;
             const long blocks = (per_phase + TO - 1) / TO;
-            const size_t smem = 4 * (size_t)(((TO + c.NP + 1) / kCR + 2) * (kCR + 4));
+            const size_t smem = 4 * (size_t)corr_lds_words((int)c.NP);
             hipLaunchKernelGGL(corr_eval_dot2, dim3((unsigned)blocks, c.S), dim3(kCBlock), smem, s, d_in, n, sb, se,
                                hist, c.d_ptaps, (int)c.N, (int)c.NP, (int)c.S, cs, c.d_corr, c.d_en,
                                (const unsigned *)c.d_best);

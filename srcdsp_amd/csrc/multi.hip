@@ -33,6 +33,10 @@ struct srcdsp_comm {
     std::vector<int> devs;
     std::vector<ncclComm_t> comms;
     std::vector<hipStream_t> streams;
+    // per rank: the events of srcdsp_comm_wait_stream / srcdsp_comm_signal_stream
+    // (record + wait pairs, serialised by order_mu)
+    std::vector<hipEvent_t> wait_ev, signal_ev;
+    std::mutex order_mu;
     // the caller's reference plus one per sharded handle built on it: the
     // communicator is released when the last of them goes, whatever the order
     // of srcdsp_comm_destroy and srcdsp_decim_sharded_destroy (atomic: handles
@@ -106,15 +110,27 @@ void comm_release(srcdsp_comm *c) {
             (void)hipStreamSynchronize(c->streams[r]);
             (void)hipStreamDestroy(c->streams[r]);
         }
+        if (r < c->wait_ev.size() && c->wait_ev[r]) (void)hipEventDestroy(c->wait_ev[r]);
+        if (r < c->signal_ev.size() && c->signal_ev[r]) (void)hipEventDestroy(c->signal_ev[r]);
         if (r < c->comms.size() && c->comms[r]) (void)rccl().CommDestroy(c->comms[r]);
     }
     if (saved >= 0) (void)hipSetDevice(saved);
     delete c;
 }
 
+// A communicator whose ranks share a device is refused, as RCCL refuses it.
+// Only a TEST build of this file (-DSRCDSP_TEST_SHARED_DEVICES, built by
+// srcdsp_amd.build.build_test_probes into tests/_build/, never shipped)
+// lets tests/test_sharded_stub.py rehearse ndev > 1 on one GPU through the
+// test-only communicator library tests/rccl_stub, opting in with the
+// environment variable SRCDSP_COMM_SHARED_DEVICES=1.
 bool shared_devices_allowed() {
+#ifdef SRCDSP_TEST_SHARED_DEVICES
     const char *v = std::getenv("SRCDSP_COMM_SHARED_DEVICES");
     return v && std::strcmp(v, "1") == 0;
+#else
+    return false;
+#endif
 }
 
 // restores the caller's current device on scope exit
@@ -138,9 +154,8 @@ SRCDSP_API int srcdsp_comm_create(srcdsp_comm_t *out, int ndev, const int *devs)
     for (int r = 0; r < ndev; ++r) {
         d[r] = devs ? devs[r] : r;
         SRCDSP_ARG_CHECK(d[r] >= 0 && d[r] < have, "comm_create: device id out of range");
-        // RCCL refuses a communicator whose ranks share a device; a rehearsal
-        // of the multi-device logic on one GPU (a communicator library that
-        // allows it, tests/rccl_stub) opts in with SRCDSP_COMM_SHARED_DEVICES=1
+        // RCCL refuses a communicator whose ranks share a device (see
+        // shared_devices_allowed for the test build that rehearses it)
         if (!shared_devices_allowed())
             for (int q = 0; q < r; ++q) SRCDSP_ARG_CHECK(d[q] != d[r], "comm_create: a device listed twice");
     }
@@ -160,9 +175,13 @@ SRCDSP_API int srcdsp_comm_create(srcdsp_comm_t *out, int ndev, const int *devs)
         return SRCDSP_ERR_HIP;
     }
     c->streams.assign(ndev, nullptr);
+    c->wait_ev.assign(ndev, nullptr);
+    c->signal_ev.assign(ndev, nullptr);
     for (int r = 0; r < ndev; ++r) {
         hipError_t e = hipSetDevice(c->devs[r]);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->streams[r], hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->wait_ev[r], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->signal_ev[r], hipEventDisableTiming);
         if (e != hipSuccess) {
             set_error(std::string("comm_create: stream on device: ") + hipGetErrorString(e));
             srcdsp_comm_destroy(c);
@@ -200,6 +219,33 @@ SRCDSP_API int srcdsp_comm_synchronize(srcdsp_comm_t c) {
         SRCDSP_HIP_TRY(hipSetDevice(c->devs[r]));
         SRCDSP_HIP_TRY(hipStreamSynchronize(c->streams[r]));
     }
+    return SRCDSP_OK;
+}
+
+// Ordering with caller streams.  The comm streams are non-blocking: they do
+// not wait for the null stream or any stream of the caller, so caller work on
+// d_in / d_out / d_root is ordered only through these two calls (or
+// srcdsp_comm_synchronize).  Each is one event record on one stream and one
+// wait on the other, on rank's device; nothing blocks the host.
+SRCDSP_API int srcdsp_comm_wait_stream(srcdsp_comm_t c, int rank, void *stream) {
+    SRCDSP_ARG_CHECK(c != nullptr, "comm_wait_stream: null comm");
+    SRCDSP_ARG_CHECK(rank >= 0 && rank < (int)c->devs.size(), "comm_wait_stream: rank out of range");
+    DeviceGuard g;
+    std::lock_guard<std::mutex> lk(c->order_mu);
+    SRCDSP_HIP_TRY(hipSetDevice(c->devs[rank]));
+    SRCDSP_HIP_TRY(hipEventRecord(c->wait_ev[rank], (hipStream_t)stream));
+    SRCDSP_HIP_TRY(hipStreamWaitEvent(c->streams[rank], c->wait_ev[rank], 0));
+    return SRCDSP_OK;
+}
+
+SRCDSP_API int srcdsp_comm_signal_stream(srcdsp_comm_t c, int rank, void *stream) {
+    SRCDSP_ARG_CHECK(c != nullptr, "comm_signal_stream: null comm");
+    SRCDSP_ARG_CHECK(rank >= 0 && rank < (int)c->devs.size(), "comm_signal_stream: rank out of range");
+    DeviceGuard g;
+    std::lock_guard<std::mutex> lk(c->order_mu);
+    SRCDSP_HIP_TRY(hipSetDevice(c->devs[rank]));
+    SRCDSP_HIP_TRY(hipEventRecord(c->signal_ev[rank], c->streams[rank]));
+    SRCDSP_HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, c->signal_ev[rank], 0));
     return SRCDSP_OK;
 }
 

@@ -10,7 +10,11 @@
 // out.bin: tag 100+ch = channel ch by the host-vector step() in two chained
 //          calls; tag 200 = all channels by the device step() after reset(),
 //          gathered to rank ROOT's device (channel-major; ROOT from the
-//          environment variable SHARDED_ROOT, default 0).
+//          environment variable SHARDED_ROOT, default 0); 201 = strided
+//          rows; 202 = an operator outliving its communicator; 203 = inputs
+//          filled and the gather target cleared and read back on the CALLER's
+//          own streams, ordered with comm.waitFor / comm.signal only (no
+//          synchronize() of the comm).
 #include <hip/hip_runtime.h>
 
 #include <complex>
@@ -162,6 +166,46 @@ int main(int argc, char **argv) {
         HIP_OK(hipMemcpy(all.data(), d_root, all.size() * sizeof(cf32), hipMemcpyDeviceToHost));
         put(out, 202, all.data(), (int64_t)(all.size() * sizeof(cf32)));
         delete g2;
+    }
+    // caller streams (the ordering rule of sharded_filters.h): the caller fills
+    // fresh input buffers and clears the gather target on streams of its own,
+    // hands them to the comm streams with waitFor, and reads the gathered rows
+    // back on its root stream after signal -- no comm.synchronize()
+    {
+        f.reset();
+        std::vector<hipStream_t> cs(R);
+        std::vector<const cf32 *> d_in3(R);
+        for (int r = 0; r < R; ++r) {
+            int first, count;
+            f.partition(r, first, count);
+            HIP_OK(hipSetDevice(devs[r]));
+            HIP_OK(hipStreamCreateWithFlags(&cs[r], hipStreamNonBlocking));
+            cf32 *x = nullptr;
+            HIP_OK(hipMalloc(&x, std::max<size_t>(1, count * n) * sizeof(cf32)));
+            HIP_OK(hipMemsetAsync(x, 0x7f, std::max<size_t>(1, count * n) * sizeof(cf32), cs[r]));
+            if (count > 0)
+                HIP_OK(hipMemcpyAsync(x, d_in[r], count * n * sizeof(cf32), hipMemcpyDeviceToDevice, cs[r]));
+            d_in3[r] = x;
+        }
+        HIP_OK(hipSetDevice(devs[root]));
+        HIP_OK(hipMemsetAsync(d_root, 0x55, (size_t)C * n_out * sizeof(cf32), cs[root]));
+        for (int r = 0; r < R; ++r) comm.waitFor(r, (void *)cs[r]);
+        f.step(d_in3, n, d_out, n_out, n);
+        f.gather(d_out, n_out, n_out, d_root, root);
+        comm.signal(root, (void *)cs[root]);
+        cf32 *h_all = nullptr;
+        HIP_OK(hipSetDevice(devs[root]));
+        HIP_OK(hipHostMalloc((void **)&h_all, all.size() * sizeof(cf32), 0));
+        HIP_OK(hipMemcpyAsync(h_all, d_root, all.size() * sizeof(cf32), hipMemcpyDeviceToHost, cs[root]));
+        HIP_OK(hipStreamSynchronize(cs[root]));
+        put(out, 203, h_all, (int64_t)(all.size() * sizeof(cf32)));
+        HIP_OK(hipHostFree(h_all));
+        comm.synchronize();  // before the buffers go
+        for (int r = 0; r < R; ++r) {
+            HIP_OK(hipSetDevice(devs[r]));
+            HIP_OK(hipStreamDestroy(cs[r]));
+            HIP_OK(hipFree((void *)d_in3[r]));
+        }
     }
     for (int r = 0; r < R; ++r) {
         HIP_OK(hipSetDevice(devs[r]));

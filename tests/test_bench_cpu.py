@@ -58,36 +58,58 @@ def test_host_cores_reports_share():
 
 
 def test_channel_layout_matches_baseline_configs():
-    """N = 1 is configs[1] (one 2^28 channel); N > 1 is configs[2]'s layout,
-    8 channels of 2^28 per GPU (64 over 8 GPUs) with a 32 GiB gather at N = 8."""
-    a = types.SimpleNamespace(workload="decim", samples=None, channels_per_gpu=None)
+    """The main series holds the same per-GPU work at every N: one 2^28
+    channel per GPU (configs[1] at N = 1), so SCALE's 1/2/4/8 values are weak
+    scaling on one layout.  configs[2]'s share (8 x 2^28 per GPU, 64 over 8
+    GPUs, 32 GiB gather at N = 8) is measured beside it at every N, and only
+    N = 8 is labelled configs[2]."""
+    a = types.SimpleNamespace(workload="decim", samples=None, channels_per_gpu=None, no_share=False)
     one = bench.channel_layout(a, 1)
-    assert one == {"channels_per_gpu": 1, "channels_total": 1, "samples_per_channel": 1 << 28, "gather_bytes": 0}
+    assert one == {"channels_per_gpu": 1, "channels_total": 1, "samples_per_channel": 1 << 28,
+                   "baseline_config": "configs[1]"}
     for n in (2, 4, 8):
         lay = bench.channel_layout(a, n)
-        assert lay["channels_per_gpu"] == 8 and lay["channels_total"] == 8 * n
-        assert lay["gather_bytes"] == 8 * n * (1 << 26) * 8
-    assert bench.channel_layout(a, 8)["gather_bytes"] == 32 << 30
-    a.channels_per_gpu = 1
-    assert bench.channel_layout(a, 8)["channels_total"] == 8
-    c = types.SimpleNamespace(workload="corr", samples=1 << 26, channels_per_gpu=None)
-    assert bench.channel_layout(c, 8)["channels_per_gpu"] == 1 and bench.channel_layout(c, 8)["gather_bytes"] == 0
+        assert lay["channels_per_gpu"] == 1 and lay["channels_total"] == n
+        assert lay["baseline_config"] == f"configs[1] on each of {n} GPUs ({n} independent channels)"
+    labels = {1: "configs[2] per-GPU layout (8 of 64 channels)", 2: "configs[2] per-GPU layout (16 of 64 channels)",
+              4: "configs[2] per-GPU layout (32 of 64 channels)", 8: "configs[2]"}
+    for n, want in labels.items():
+        sh = bench.share_layout(a, n)
+        assert sh["channels_per_gpu"] == 8 and sh["channels_total"] == 8 * n and sh["baseline_config"] == want
+        assert sh["gather_bytes"] == (8 * n * (1 << 26) * 8 if n > 1 else 0)
+    assert bench.share_layout(a, 8)["gather_bytes"] == 32 << 30
+    a.channels_per_gpu = 8  # an explicit layout becomes the main series, no share beside it
+    assert bench.channel_layout(a, 8)["baseline_config"] == "configs[2]"
+    assert bench.channel_layout(a, 4)["baseline_config"] == "configs[2] per-GPU layout (32 of 64 channels)"
+    assert bench.share_layout(a, 8) is None
+    a.channels_per_gpu = 3
+    assert bench.channel_layout(a, 2)["baseline_config"] == "custom"
+    c = types.SimpleNamespace(workload="corr", samples=1 << 26, channels_per_gpu=None, no_share=False)
+    assert bench.channel_layout(c, 8)["channels_per_gpu"] == 1 and bench.channel_layout(c, 8)["baseline_config"] is None
+    assert bench.share_layout(c, 8) is None
 
 
-def test_gpus8_dry_run_world_and_layout():
-    """`bench.py --gpus 8 --dry-run`, the driver's N = 8 command with no GPU
-    touched: 8 ranks assemble one gloo world, and every rank holds configs[2]'s
-    layout (8 x 2^28-sample channels per rank, 64 in all, 32 GiB gather)."""
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_gpus_n_dry_run_world_and_labels(n):
+    """`bench.py --gpus N --dry-run`, the driver's N-GPU command with no GPU
+    touched: N ranks assemble one gloo world; every rank holds the main
+    series' layout (one 2^28 channel per GPU) and configs[2]'s share, labelled
+    configs[2] only at N = 8."""
     import json
     import subprocess
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env["OMP_NUM_THREADS"] = "1"
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--dry-run"],
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--dry-run"],
                        capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
-    assert sorted(l["rank"] for l in lines) == list(range(8))
+    assert sorted(l["rank"] for l in lines) == list(range(n))
     for l in lines:
-        assert l["world"] == 8 and l["world_seen"] == 8
-        assert l["layout"] == {"channels_per_gpu": 8, "channels_total": 64, "samples_per_channel": 1 << 28,
-                               "gather_bytes": 32 << 30}
+        assert l["world"] == n and l["world_seen"] == n
+        assert l["layout"] == {"channels_per_gpu": 1, "channels_total": n, "samples_per_channel": 1 << 28,
+                               "baseline_config": f"configs[1] on each of {n} GPUs ({n} independent channels)"}
+        sh = l["share_layout"]
+        assert sh["channels_per_gpu"] == 8 and sh["channels_total"] == 8 * n
+        assert sh["gather_bytes"] == 8 * n * (1 << 26) * 8
+        assert sh["baseline_config"] == ("configs[2]" if n == 8 else
+                                         f"configs[2] per-GPU layout ({8 * n} of 64 channels)")

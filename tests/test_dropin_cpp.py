@@ -244,6 +244,7 @@ def test_sharded_program_matches_oracle(tmp_path):
     assert got[200] == np.concatenate(alls).tobytes()
     assert got[201] == got[200]  # strided rows through the Memcpy2D branch of the gather
     assert got[202] == got[200]  # operator outliving its GpuComm
+    assert got[203] == got[200]  # caller streams ordered by waitFor / signal (real RCCL, one rank)
 
 
 @pytest.mark.gpu

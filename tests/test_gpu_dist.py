@@ -85,9 +85,10 @@ def test_two_ranks_on_gpu_match_single_process(tmp_path, pat_at):
 def test_bench_two_rank_rehearsal_default_layout():
     """`bench.py --gpus 2` as the driver runs it, both ranks on cuda:0
     (collectives rehearsed over gloo: two ranks on one device cannot form an
-    RCCL communicator): the default N > 1 layout is configs[2]'s, 8 channels
-    of 2^28 samples per rank, and the timed gather moves all 16 channels'
-    outputs (8 GiB) to rank 0."""
+    RCCL communicator): the main series is one 2^28 channel per rank (the
+    N = 1 line's work per GPU, weak scaling); `configs2_share` beside it runs
+    8 channels per rank, labelled as configs[2]'s per-GPU layout (16 of 64),
+    and its timed gather moves all 16 channels' outputs (8 GiB) to rank 0."""
     import json
     import torch
     if torch.cuda.device_count() < 1:
@@ -102,8 +103,14 @@ def test_bench_two_rank_rehearsal_default_layout():
     line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["world_size_reported"] == 2 and line["backend"] == "gloo"
     cfg = line["config"]
-    assert cfg["channels_per_gpu"] == 8 and cfg["channels_total"] == 16 and cfg["baseline_config"] == "configs[2]"
+    assert cfg["channels_per_gpu"] == 1 and cfg["channels_total"] == 2
+    assert cfg["baseline_config"] == "configs[1] on each of 2 GPUs (2 independent channels)"
     assert cfg["samples_per_channel"] == 1 << 28
-    assert line["gather_bytes"] == 16 * (1 << 26) * 8 and line["gather_ms"] > 0
-    assert line["roofline"]["per_gpu"] and line["roofline"]["channels_per_launch"] == 8
-    assert line["roofline"]["algorithmic_bytes_per_launch"] == 8 * (1 << 28) * 10
+    assert line["roofline"]["per_gpu"] and line["roofline"]["channels_per_launch"] == 1
+    assert line["roofline"]["algorithmic_bytes_per_launch"] == (1 << 28) * 10
+    sh = line["configs2_share"]
+    assert sh["baseline_config"] == "configs[2] per-GPU layout (16 of 64 channels)"
+    assert sh["channels_per_gpu"] == 8 and sh["channels_total"] == 16 and sh["value"] > 0
+    assert sh["gather_bytes"] == 16 * (1 << 26) * 8 and sh["gather_ms"] > 0
+    assert sh["roofline"]["channels_per_launch"] == 8
+    assert sh["roofline"]["algorithmic_bytes_per_launch"] == 8 * (1 << 28) * 10

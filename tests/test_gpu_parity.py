@@ -579,11 +579,13 @@ def test_decim_errors_and_empty(S):
         d2.setCoeffs(np.ones(7, np.float32))  # dsptl_dnsampling_filters.h:122 assert
 
 
-def test_headline_size_properties(S, O):
-    """Config 2 at full size (2^28 samples, device-resident): spot-check output
-    windows against the oracle run on the same input windows (first tiles,
-    tile seams, random interior, last tile) -- size-independent parity."""
+def test_headline_whole_output(S, O):
+    """Config 2 at full size (2^28 complex<float> samples, device-resident, one
+    step()): EVERY one of the 2^26 outputs against the oracle (FMA contract),
+    run in parallel windows on the host (tests/fullsize.py); the device
+    generator equals the host one on the first, a seam and the last window."""
     import torch
+    import fullsize as F
     from srcdsp_amd.design import hamming_sinc
     c = hamming_sinc(127)
     L = 1 << 28
@@ -591,32 +593,24 @@ def test_headline_size_properties(S, O):
     S.fill_synthetic(x, "cf32", seed=0x5EED, channel=0)
     y = S.FilterDnsamplingFir(c, 4, fp="fma").step(x)
     torch.cuda.synchronize()
-    rng = np.random.default_rng(1)
-    n_out = L // 4
-    starts = [0, 2048 - 3, 4096 - 3, n_out - 1000] + list(rng.integers(40, n_out - 1000, 12))
-    for s0 in starts:
-        s0 = int(s0)
-        lo = max(0, 4 * s0 - 128)
-        xin = x[lo:4 * (s0 + 64)].cpu().numpy()
-        host = O["fma"].gen_cf32(0x5EED, 0, lo, len(xin))
-        assert np.array_equal(xin, host)  # device generator == host generator
-        ref = O["fma"].decim(0, 4, c)
-        pre = (4 * s0 - lo) // 4
-        r = ref.step(xin)[pre:]
-        got = y[s0:s0 + 64].cpu().numpy()
-        assert np.array_equal(got, r[:len(got)]), s0
+    xh = x.cpu().numpy()
+    for lo in (0, (1 << 27) - 5000, L - 8192):
+        assert np.array_equal(xh[lo:lo + 8192], O["fma"].gen_cf32(0x5EED, 0, lo, 8192)), lo
+    want = F.decim_all(lambda: O["fma"].decim(0, 4, c), xh, 4, 128, np.empty(L // 4, np.complex64))
+    bad = F.first_bad(y.cpu().numpy(), want)
+    assert bad is None, f"first differing output {bad}"
     del x, y
     torch.cuda.empty_cache()
 
 
-def test_config3_per_gpu_share_size_properties(S, O):
+def test_config3_per_gpu_share_whole_channel(S, O):
     """Config 3's per-GPU share at full size: 8 channels x 2^28 complex<float>
-    samples (channels 8..15 of the 64, i.e. rank 1 of 8), one batched launch
-    (grid.y = channel), as bench.py --gpus N steps it.  Spot windows of every
-    channel (first tiles, tile seams, random interior, last tile) against the
-    oracle on the same input windows; the device generator is checked against
-    the host one on each window."""
+    samples (channels 8..15 of the 64, i.e. rank 1 of 8), one batched step as
+    bench.py --gpus N runs it.  One whole channel (all 2^26 outputs) against
+    the oracle; spot windows of the seven others (first tiles, a seam, random
+    interior, last tile); each channel's history is its own tail."""
     import torch
+    import fullsize as F
     from srcdsp_amd.design import hamming_sinc
     c = hamming_sinc(127)
     C, L = 8, 1 << 28
@@ -628,9 +622,17 @@ def test_config3_per_gpu_share_size_properties(S, O):
     fs = [S.FilterDnsamplingFir(c, 4, fp="fma") for _ in range(C)]
     S.decim_step_batched(fs, x, y)
     torch.cuda.synchronize()
+    full = 5  # channel 13
+    xh = x[full].cpu().numpy()
+    want = F.decim_all(lambda: O["fma"].decim(0, 4, c), xh, 4, 128, np.empty(L // 4, np.complex64))
+    bad = F.first_bad(y[full].cpu().numpy(), want)
+    assert bad is None, f"channel {ch0 + full}: first differing output {bad}"
+    del xh, want
     rng = np.random.default_rng(3)
     n_out = L // 4
     for k in range(C):
+        if k == full:
+            continue
         starts = [0, 2048 - 3, n_out - 1000] + list(rng.integers(40, n_out - 1000, 3))
         for s0 in starts:
             s0 = int(s0)
@@ -648,15 +650,14 @@ def test_config3_per_gpu_share_size_properties(S, O):
     torch.cuda.empty_cache()
 
 
-def test_config4_size_properties(S, O):
+def test_config4_whole_output(S, O):
     """Config 4 at full size (2^28 complex<int16_t>, device-resident, one fused
-    mixer -> decimator step): output windows (first tile, tile seams, random
-    interior, last tile) against the reference pair run on the same input
-    windows.  The oracle mixer is advanced to each window start by stepping
-    zeros (the phase does not depend on the data), so the NCO phase is checked
-    across the whole 2^28-sample call, and the oracle decimator starts each
-    window 128 samples early with an empty history."""
+    mixer -> decimator step): EVERY output against the reference pair -- the
+    oracle mixer over the whole call (so the NCO phase is checked across all
+    2^28 samples), then the oracle decimator over the mixed stream in parallel
+    windows started 128 samples early with an empty history."""
     import torch
+    import fullsize as F
     from srcdsp_amd.design import hamming_sinc, q14
     cq = q14(hamming_sinc(127))
     L = 1 << 28
@@ -667,30 +668,17 @@ def test_config4_size_properties(S, O):
     d = S.FilterDnsamplingFir(cq, 4, "complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int32_t")
     y = S.MixerDecimatorChain(m, d).step(x)
     torch.cuda.synchronize()
+    xh = x.cpu().numpy()
+    for lo in (0, L - 8192):
+        assert np.array_equal(xh[lo:lo + 8192], O["strict"].gen_ci16(0x5EED, 0, lo, 8192, -8192, 8191)), lo
     om = O["strict"].mixer(4096)
     om.reset(0.1)
-    n_out, TO = L // 4, 2048
-    rng = np.random.default_rng(4)
-    starts = sorted({0, 40, TO - 3, 2 * TO - 3, 7 * TO + 5, n_out - 1000, *map(int, rng.integers(64, n_out - 1000, 10))})
-    zeros = np.zeros((1 << 22, 2), np.int16)
-    pos = 0  # samples the oracle mixer has consumed
-    for s0 in starts:
-        lo = max(0, 4 * s0 - 128)
-        hi = 4 * (s0 + 64)
-        if lo < pos:  # overlapping windows: take the next one from where the mixer is
-            continue
-        while pos < lo:
-            k = min(lo - pos, len(zeros))
-            om.step(zeros[:k])
-            pos += k
-        xin = x[lo:hi].cpu().numpy()
-        assert np.array_equal(xin, O["strict"].gen_ci16(0x5EED, 0, lo, hi - lo, -8192, 8191))
-        mixed = om.step(xin)
-        pos = hi
-        od = O["strict"].decim(1, 4, cq)
-        r = od.step(mixed)[(4 * s0 - lo) // 4:]
-        got = y[s0:s0 + 64].cpu().numpy()
-        assert np.array_equal(got, r[:len(got)]), s0
+    mixed = om.step(xh)
+    assert m.state()[:2] == om.state()[:2]  # the phase after the call
+    del xh
+    want = F.decim_all(lambda: O["strict"].decim(1, 4, cq), mixed, 4, 128, np.empty((L // 4, 2), np.int16))
+    bad = F.first_bad(y.cpu().numpy(), want)
+    assert bad is None, f"first differing output {bad}"
     del x, y
     torch.cuda.empty_cache()
 
@@ -1000,14 +988,13 @@ def test_correlator_long_window_vs_oracle(S, O, N, S_, n, chunk):
     assert events >= 1
 
 
-def test_config5_size_properties(S, O):
+def test_config5_whole_buffer(S, O):
     """Config 5 at full size (2^26 samples, device-resident, one step): the
     bench's buffer (noise +-125, the 1024-sample QPSK pattern x2 at 3/4).  The
-    GPU scan's first detection, bitSamples and registers equal the reference's
-    on a window around the hit, the reference primed with the samples before
-    the window (the registers after a detection-free stream depend only on the
-    last N*S+2 samples)."""
-    from srcdsp_amd import dist as D
+    oracle scans the WHOLE buffer (parallel windows, each primed with its
+    N*S+2-sample halo: tests/fullsize.py): no detection before the GPU's, the
+    same index, and equal bitSamples and registers there."""
+    import fullsize as F
     from srcdsp_amd.design import qpsk_pattern
     L = 1 << 26
     p = qpsk_pattern(1024, 500, seed=2)
@@ -1019,15 +1006,17 @@ def test_config5_size_properties(S, O):
     g = S.FixedPatternCorrelator(1024, 1)
     g.setPattern(p)
     fg, ig = g.step(dev(x))
-    r = O["fma"].corr(1024, 1)
-    r.set_pattern(p)
-    w0 = off - 4096
-    r.prime(x[w0 - D.corr_halo(1024, 1):w0])
-    fr, ir = r.step(x[w0:w0 + 8192])
-    assert fg and fr and ig == w0 + ir
-    assert np.array_equal(g.getRefBitSamples(), r.bit_samples())
-    st, sr = g.getStatus(), r.status()
-    assert all(st[k] == sr[k] for k in ("energy", "corr", "coeffs_energy", "coeff_scaling"))
+
+    def make():
+        r = O["fma"].corr(1024, 1)
+        r.set_pattern(p)
+        return r
+
+    fr, ir, bits, st_r = F.corr_first(make, x, 1024, 1, win=1 << 19)
+    assert fg and fr and ig == ir, (fg, ig, fr, ir)
+    assert np.array_equal(g.getRefBitSamples(), bits)
+    st = g.getStatus()
+    assert all(st[k] == st_r[k] for k in ("energy", "corr", "coeffs_energy", "coeff_scaling"))
 
 
 def test_time_split_segments_equal_single_call(S, O):

@@ -5,7 +5,11 @@ tests/cpp/sharded_main.cpp drives dsptl::ShardedDnsamplingFir over a
 communicator whose ranks all name device 0.  Real RCCL refuses that, so the
 child process loads tests/rccl_stub (a test-only librccl.so.1: grouped
 Gather / Send / Recv as stream-ordered device copies) through LD_LIBRARY_PATH,
-and opts in to shared devices with SRCDSP_COMM_SHARED_DEVICES=1.  What runs is
+and links the test build of the library whose multi.hip honours
+SRCDSP_COMM_SHARED_DEVICES=1 (tests/_build/shared_dev/libsrcdsp_hip.so: the
+product objects with multi.hip compiled -DSRCDSP_TEST_SHARED_DEVICES; the
+shipped library refuses a device listed twice whatever the environment says).
+What runs is
 the product's own multi-device code: the block partition, one host thread
 per rank in step_host, one batched launch per rank on its comm stream, the
 even-partition ncclGather, and for uneven or strided rows the root's
@@ -20,10 +24,11 @@ import subprocess
 import numpy as np
 import pytest
 
-from test_dropin_cpp import INC, LIBDIR, ROOT, _read, _rec
+from test_dropin_cpp import INC, ROOT, _read, _rec
 
 pytestmark = pytest.mark.gpu
 STUB = os.path.join(ROOT, "tests", "rccl_stub", "rccl_stub.cpp")
+SHARED_DEV_DIR = os.path.join(ROOT, "tests", "_build", "shared_dev")
 HIPFLAGS = ["-D__HIP_PLATFORM_AMD__", "-I", "/opt/rocm/include"]
 
 
@@ -38,9 +43,11 @@ def built(tmp_path_factory):
                         "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     exe = str(d / "sharded_main")
+    assert os.path.exists(os.path.join(SHARED_DEV_DIR, "libsrcdsp_hip.so")), \
+        "tests/_build/shared_dev not built: run python -c 'import __graft_entry__ as g; g.build()'"
     r = subprocess.run(["g++", "-std=c++14", "-O2", *HIPFLAGS, "-I", INC,
-                        os.path.join(ROOT, "tests", "cpp", "sharded_main.cpp"), "-o", exe, "-L", LIBDIR,
-                        "-lsrcdsp_hip", "-L/opt/rocm/lib", "-lamdhip64", f"-Wl,-rpath,{LIBDIR}",
+                        os.path.join(ROOT, "tests", "cpp", "sharded_main.cpp"), "-o", exe, "-L", SHARED_DEV_DIR,
+                        "-lsrcdsp_hip", "-L/opt/rocm/lib", "-lamdhip64", f"-Wl,-rpath,{SHARED_DEV_DIR}",
                         "-Wl,-rpath,/opt/rocm/lib"], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     return str(d), exe
@@ -92,6 +99,7 @@ def test_sharded_decim_ndev_on_one_gpu(built, tmp_path, ndev, C, root):
     assert got[200] == want
     assert got[201] == want  # strided rows: root's hipMemcpy2DAsync + per-row ncclSend/ncclRecv
     assert got[202] == want  # operator outliving its communicator
+    assert got[203] == want  # caller streams ordered by waitFor / signal, no synchronize()
     q, rem = divmod(C, ndev)
     transfers = [l for l in r.stderr.splitlines() if l.startswith("rccl_stub:")]
     if rem == 0:
@@ -104,11 +112,12 @@ def test_sharded_decim_ndev_on_one_gpu(built, tmp_path, ndev, C, root):
         assert len(transfers) == 2 * nonroot_ranks + nonroot_rows
 
 
-def test_shared_devices_refused_by_default(S, monkeypatch):
-    """Without the opt-in a device listed twice is refused before any
-    communicator is made (real RCCL would refuse it too)."""
+def test_shared_devices_refused_by_the_product(S, monkeypatch):
+    """The shipped library refuses a device listed twice before any
+    communicator is made (as real RCCL would), even with the test build's
+    opt-in variable set: the knob exists only in tests/_build/shared_dev."""
     import ctypes as C
-    monkeypatch.delenv("SRCDSP_COMM_SHARED_DEVICES", raising=False)
+    monkeypatch.setenv("SRCDSP_COMM_SHARED_DEVICES", "1")
     lib = S.lib()
     h = C.c_void_p()
     devs = (C.c_int * 2)(0, 0)
