@@ -214,6 +214,16 @@ SRCDSP_API int srcdsp_corr_step_host(srcdsp_corr_t h, const void *in, size_t n, 
  * (correlators.h:221-250 without :262-291): history ring and the
  * energy/correlation registers.  Seeds a time segment with its halo. */
 SRCDSP_API int srcdsp_corr_prime(srcdsp_corr_t h, const void *d_in, size_t n, void *stream);
+/* step() as built with CREATE_DEBUG_FILES (correlators.h:107-132, 253-257):
+ * also returns, for every sample the call processed, the registers the
+ * reference writes to its debug files -- corr_out[k] = corrValue[0] and
+ * energy_out[k] = energyValue[0] after input sample k (host arrays of n
+ * entries; *count = corrIndex + 2 on a detection, else n).  Runs the
+ * segmented kernels (they keep per-sample values); same results as step(). */
+SRCDSP_API int srcdsp_corr_step_trace(srcdsp_corr_t h, const void *d_in, size_t n, int *found, int *corr_index,
+                                      uint32_t *corr_out, uint32_t *energy_out, size_t *count, void *stream);
+SRCDSP_API int srcdsp_corr_step_host_trace(srcdsp_corr_t h, const void *in, size_t n, int *found, int *corr_index,
+                                           uint32_t *corr_out, uint32_t *energy_out, size_t *count);
 /* getRefBitSamples  correlators.h:311-316 (N complex<int16_t>, host copy) */
 SRCDSP_API int srcdsp_corr_get_bit_samples(srcdsp_corr_t h, int16_t *bits_host);
 /* getStatus  correlators.h:90 (CorrState fields) */

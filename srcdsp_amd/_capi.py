@@ -69,6 +69,8 @@ SIGNATURES = {
     "srcdsp_corr_step": (I, [VP, VP, SZ, IP, IP, VP]),
     "srcdsp_corr_prime": (I, [VP, VP, SZ, VP]),
     "srcdsp_corr_step_host": (I, [VP, VP, SZ, IP, IP]),
+    "srcdsp_corr_step_trace": (I, [VP, VP, SZ, IP, IP, U32P, U32P, C.POINTER(C.c_size_t), VP]),
+    "srcdsp_corr_step_host_trace": (I, [VP, VP, SZ, IP, IP, U32P, U32P, C.POINTER(C.c_size_t)]),
     "srcdsp_corr_get_bit_samples": (I, [VP, I16P]),
     "srcdsp_corr_get_status": (I, [VP, U32P, U32P, U32P, IP, DP]),
     "srcdsp_fifo_create": (I, [HP, SZ, SZ, D]),

@@ -577,9 +577,19 @@ static int corr_alloc_scratch(srcdsp_corr_state &c, size_t n) {
 
 // detect = false: stream the samples with no detection test (corr_prime):
 // only the last three positions are evaluated (they feed the registers).
+// trace (CREATE_DEBUG_FILES, correlators.h:253-257): host arrays of n_
+// entries receive corrValue[0] / energyValue[0] after each processed sample
+// (*trace_n of them: corrIndex + 2 on a detection, else n_); the segmented
+// kernels run, since only they keep per-sample values.
+struct CorrTrace {
+    uint32_t *corr = nullptr, *energy = nullptr;
+    size_t *count = nullptr;
+};
+
 static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *found, int *corr_index,
-                    hipStream_t s, bool detect = true) {
+                    hipStream_t s, bool detect = true, const CorrTrace *trace = nullptr) {
     *found = 0;
+    if (trace) *trace->count = 0;
     if (n_ == 0) return SRCDSP_OK;
     const long n = (long)n_;
     if (n > 0x7fffffffL) {
@@ -601,7 +611,7 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
     // the fused scan keeps no per-sample values (corr_point computes the three
     // the registers need); the segmented kernels write corr/energy per sample
     // for corr_detect
-    const bool fused = fast && detect;
+    const bool fused = fast && detect && !trace;
     if (!fused) {
         rc = corr_alloc_scratch(c, n_);
         if (rc) return rc;
@@ -627,7 +637,7 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
     }
     // the segmented path: priming (the last 3 positions only) and the generic
     // kernels (S > 1 or N % 16 != 0)
-    for (long sb = detect ? (fast ? n : 0) : std::max(0L, n - 3); sb < n; sb += seg) {
+    for (long sb = detect ? (fused ? n : 0) : std::max(0L, n - 3); sb < n; sb += seg) {
         const long se = std::min(n, sb + seg);
         if (dot2) {  // grid.y = phase of the stride
             constexpr long TO = (long)kCBlock * kCR;
@@ -661,6 +671,12 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
 
     const bool hit = best != none;
     const long last = hit ? (long)best : n - 1;  // last processed sample
+    if (trace) {  // every processed sample's registers (the segmented kernels computed them all up to `last`)
+        SRCDSP_HIP_TRY(hipMemcpyAsync(trace->corr, c.d_corr, 4 * (size_t)(last + 1), hipMemcpyDeviceToHost, s));
+        SRCDSP_HIP_TRY(hipMemcpyAsync(trace->energy, c.d_en, 4 * (size_t)(last + 1), hipMemcpyDeviceToHost, s));
+        SRCDSP_HIP_TRY(hipStreamSynchronize(s));
+        *trace->count = (size_t)(last + 1);
+    }
     // registers after processing `last` (correlators.h:228-230, 248-250)
     uint32_t cw[3] = {0, 0, 0}, ew[3] = {0, 0, 0};
     const long lo = std::max(0L, last - 2);
@@ -889,6 +905,34 @@ SRCDSP_API int srcdsp_corr_step_host(srcdsp_corr_t h, const void *in, size_t n, 
     host_copy(c.stage.h_buf, in, 4 * n);
     SRCDSP_HIP_TRY(hipMemcpyAsync(c.stage.d_buf, c.stage.h_buf, 4 * n, hipMemcpyHostToDevice, c.stage.stream));
     return corr_run(c, (const uint32_t *)c.stage.d_buf, n, found, corr_index, c.stage.stream);
+}
+
+SRCDSP_API int srcdsp_corr_step_trace(srcdsp_corr_t h, const void *d_in, size_t n, int *found, int *corr_index,
+                                      uint32_t *corr_out, uint32_t *energy_out, size_t *count, void *stream) {
+    SRCDSP_ARG_CHECK(h != nullptr && found != nullptr && corr_index != nullptr && count != nullptr,
+                     "corr_step_trace: null argument");
+    SRCDSP_ARG_CHECK(d_in != nullptr || n == 0, "corr_step_trace: null input");
+    SRCDSP_ARG_CHECK(n == 0 || (corr_out != nullptr && energy_out != nullptr), "corr_step_trace: null trace array");
+    const CorrTrace t{corr_out, energy_out, count};
+    return corr_run(h->c, (const uint32_t *)d_in, n, found, corr_index, (hipStream_t)stream, true, &t);
+}
+
+SRCDSP_API int srcdsp_corr_step_host_trace(srcdsp_corr_t h, const void *in, size_t n, int *found, int *corr_index,
+                                           uint32_t *corr_out, uint32_t *energy_out, size_t *count) {
+    SRCDSP_ARG_CHECK(h != nullptr && found != nullptr && corr_index != nullptr && count != nullptr,
+                     "corr_step_host_trace: null argument");
+    SRCDSP_ARG_CHECK(n == 0 || (in != nullptr && corr_out != nullptr && energy_out != nullptr),
+                     "corr_step_host_trace: null argument");
+    *found = 0;
+    *count = 0;
+    if (n == 0) return SRCDSP_OK;
+    srcdsp_corr_state &c = h->c;
+    int rc = c.stage.reserve(4 * n, 4 * n);
+    if (rc) return rc;
+    host_copy(c.stage.h_buf, in, 4 * n);
+    SRCDSP_HIP_TRY(hipMemcpyAsync(c.stage.d_buf, c.stage.h_buf, 4 * n, hipMemcpyHostToDevice, c.stage.stream));
+    const CorrTrace t{corr_out, energy_out, count};
+    return corr_run(c, (const uint32_t *)c.stage.d_buf, n, found, corr_index, c.stage.stream, true, &t);
 }
 
 SRCDSP_API int srcdsp_corr_get_bit_samples(srcdsp_corr_t h, int16_t *bits) {

@@ -1384,11 +1384,20 @@ __global__ __launch_bounds__(kDtBlock) void decim_tile(DecimLaunch a) {
 //  4 (two-word sequence table stored once, Pe <= kSeq2Off): as 3 with each
 //    table held once (2 Pe words: the LDS of form 2's doubled one-word table),
 //    the granule's index m + lo (< 2 Pe) wrapped by one subtract and one min.
+//  5 (two-word sequence table stored once and ROTATED, Pe | SPT, 512 lanes):
+//    when the period divides the tile's input span (config 4: N = 4096, any
+//    frequency, Pe a power of two <= 4096), every tile's first staged sample
+//    has the same table index m0 = -HS mod Pe, so the tables are stored
+//    rotated by m0 and staged granule g = t + i BLOCK of every tile reads
+//    index (4 t + 4 i BLOCK) mod Pe = (4 t mod Pe) + (i odd ? 2048 mod Pe : 0)
+//    < Pe: two per-lane base addresses made once, no index arithmetic per
+//    granule (form 4 spends 4 VALU per granule on it).
 // Products via VOP3 dot2 and the pair clamp above.
 constexpr int kSeq2Off = 4096, kSeq2Max = kSeq2Off / 2;
 template <int NT, int BLOCK, bool MIX, int MINW, int TABM = 0, int MD = 4>
 __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
-    constexpr bool TAB2 = TABM == 1, SEQT = TABM >= 2, SEQ2 = TABM >= 3, SEQ1 = TABM == 4;
+    constexpr bool TAB2 = TABM == 1, SEQT = TABM >= 2, SEQ2 = TABM >= 3, SEQ1 = TABM == 4, SEQR = TABM == 5;
+    static_assert(!SEQR || BLOCK == 512, "the rotated table's two lane bases assume 4 BLOCK = 2048 samples per round");
     constexpr bool RT = NT == 0;                  // the tap count at run time (a.ntaps <= kDot2MaxTaps)
     static_assert(MD == 1 || MD == 2 || MD == 4 || MD == 8 || MD == 16, "M dividing the 16-sample lane chunk");
     static_assert(MD == 4 || RT, "tap counts are compiled in at M = 4 only");
@@ -1439,11 +1448,14 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     const unsigned Pe = SEQT ? a.mix_pe : 1u;
     if constexpr (MIX) {
         const int16_t *tab = a.mix_table;
-        const int nw = SEQ1 ? (int)Pe : SEQT ? 2 * (int)Pe : (TAB2 ? 2 : 1) * (int)N;
+        const int nw = (SEQ1 || SEQR) ? (int)Pe : SEQT ? 2 * (int)Pe : (TAB2 ? 2 : 1) * (int)N;
+        // SEQR: entry j is the sample j - HS (mod Pe) of every tile's staging
+        const unsigned rot = SEQR ? (unsigned)((long)Pe - (long)HS % (long)Pe) % Pe : 0u;
         for (int i = t; i < nw; i += BLOCK) {
             unsigned k;
             if constexpr (SEQT) {
-                const unsigned m = (unsigned)i < Pe ? (unsigned)i : (unsigned)i - Pe;
+                unsigned m = (unsigned)i < Pe ? (unsigned)i : (unsigned)i - Pe;
+                if constexpr (SEQR) m = (m + rot) % Pe;
                 k = (unsigned)(((unsigned long)a.mix_phase0 + (unsigned long)m * fr) % N);
             } else {
                 k = (unsigned)i < N ? (unsigned)i : (unsigned)i - N;
@@ -1473,7 +1485,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     };
     // input sample s >= 0 of this call, mixed (any table form)
     auto mix_at = [&](uint32_t w, long s) {
-        if constexpr (SEQT) return mix1(w, (unsigned)(s % (long)Pe));
+        if constexpr (SEQR) return mix1(w, (unsigned)((s + HS) % (long)Pe));  // the table is rotated by -HS
+        else if constexpr (SEQT) return mix1(w, (unsigned)(s % (long)Pe));
         else return mix1(w, phase_add(a.mix_phase0, (unsigned)(s % (long)N)));
     };
     if (t_begin == 0 && t_end > 0) {  // new history = last H samples of (history ++ mixed input)
@@ -1572,6 +1585,20 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
         *lds_half(g, 0) = make_uint2(clamp_pair_s14(r0, r1), clamp_pair_s14(r2, r3));
         *lds_half(g, 1) = make_uint2(clamp_pair_s14(i0, i1), clamp_pair_s14(i2, i3));
     };
+    // SEQR: byte addresses of the lane's granule in even / odd rounds
+    const unsigned seqr_b0 = SEQR ? 4u * ((4u * t) % Pe) : 0u;
+    const unsigned seqr_b1 = SEQR ? 4u * ((4u * t) % Pe + 2048u % Pe) : 0u;
+    auto put_mixed_seqr = [&](int g, uint4 w, unsigned bytes) {
+        const char *tb = (const char *)ctab;
+        const uint4 A = *(const uint4 *)__builtin_assume_aligned(tb + bytes, 16);
+        const uint4 B = *(const uint4 *)__builtin_assume_aligned(tb + bytes + 4 * kSeq2Off, 16);
+        const int32_t r0 = sdot2_0(w.x, A.x), i0 = sdot2_0(w.x, B.x);
+        const int32_t r1 = sdot2_0(w.y, A.y), i1 = sdot2_0(w.y, B.y);
+        const int32_t r2 = sdot2_0(w.z, A.z), i2 = sdot2_0(w.z, B.z);
+        const int32_t r3 = sdot2_0(w.w, A.w), i3 = sdot2_0(w.w, B.w);
+        *lds_half(g, 0) = make_uint2(clamp_pair_s14(r0, r1), clamp_pair_s14(r2, r3));
+        *lds_half(g, 1) = make_uint2(clamp_pair_s14(i0, i1), clamp_pair_s14(i2, i3));
+    };
     auto put_mixed_seq = [&](int g, uint4 w, unsigned m, unsigned lo) {
         if constexpr (SEQ2) put_mixed_seq2(g, w, m, lo);
         else put_mixed_seq1(g, w, m, lo);
@@ -1579,7 +1606,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     auto advp = [&](unsigned p, unsigned d) { p += d; const unsigned q = p - Pe; return q < p ? q : p; };
     // SEQT: (4*tile*TO - HS) mod Pe of the workgroup's current tile
     unsigned m_tile = 0;
-    if constexpr (MIX && SEQT)
+    if constexpr (MIX && SEQT && !SEQR)
         if (t_begin < t_end) m_tile = (unsigned)((t_begin * (long)SPT - HS + 4 * (long)Pe * (1 + HS / 4)) % (long)Pe);
     auto put_mixed = [&](int g, uint4 w, unsigned ph) {
         if constexpr (MIX) {
@@ -1622,7 +1649,13 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
         SRCDSP_PH(ph0);
         SRCDSP_LDS_BARRIER();
         SRCDSP_PH(ph1);
-        if (MIX && SEQT && tile != 0) {
+        if (MIX && SEQR && tile != 0) {
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int g = sg(i);
+                if (g >= 0) put_mixed_seqr(g, v[i], (i & 1) ? seqr_b1 : seqr_b0);
+            }
+        } else if (MIX && SEQT && tile != 0) {
             unsigned m = m_tile;  // wave-uniform
 #pragma unroll
             for (int i = 0; i < PER; ++i) {
@@ -1655,7 +1688,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
         }
         SRCDSP_PH(ph2);
         SRCDSP_LDS_BARRIER();
-        if constexpr (MIX && SEQT) m_tile = advp(m_tile, a.mix_pe_dtile);
+        if constexpr (MIX && SEQT && !SEQR) m_tile = advp(m_tile, a.mix_pe_dtile);
         if (tile + 1 < t_end) stage_load(tile + 1);
         SRCDSP_PH(ph3);
 
@@ -1676,9 +1709,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
         };
         uint32_t w[R];
         if constexpr (!RT) {
-            int32_t yr[R], yi[R];
-#pragma unroll
-            for (int r = 0; r < R; ++r) yr[r] = yi[r] = 0;
+            int32_t yr[R], yi[R];  // started by the first tap pair's inline-0 dot2 (no v_mov)
             // window: Dr[d + OFF], d in [-(4*NG), 8), NG = granules below the lane base
             constexpr int NG = ceildiv(JC - 1, 4);
             constexpr int OFF = 4 * NG;
@@ -1704,8 +1735,13 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
                 const uint32_t P = tp[j];
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    yr[r] = sdot2(Dr[OFF + 2 * r - j], P, yr[r]);
-                    yi[r] = sdot2(Di[OFF + 2 * r - j], P, yi[r]);
+                    if (j == 0) {
+                        yr[r] = sdot2_0(Dr[OFF + 2 * r], P);
+                        yi[r] = sdot2_0(Di[OFF + 2 * r], P);
+                    } else {
+                        yr[r] = sdot2(Dr[OFF + 2 * r - j], P, yr[r]);
+                        yi[r] = sdot2(Di[OFF + 2 * r - j], P, yi[r]);
+                    }
                 }
             }
             quant(yr, yi, w, R, 1);

@@ -425,6 +425,25 @@ class FixedPatternCorrelator(_Handle):
             A.call("srcdsp_corr_step_host", self._h, _ptr(x), n, C.byref(found), C.byref(idx))
         return bool(found.value), idx.value
 
+    def step_trace(self, inp):
+        """step() as the reference's CREATE_DEBUG_FILES build runs it
+        (correlators.h:253-257): (found, corrIndex, corr, energy), where corr[k]
+        / energy[k] are corrValue[0] / energyValue[0] after each processed
+        input sample (numpy uint32)."""
+        n = _nsamples(inp, "ci16")
+        found, idx, cnt = C.c_int(0), C.c_int(-1), C.c_size_t(0)
+        corr, en = np.zeros(max(n, 1), np.uint32), np.zeros(max(n, 1), np.uint32)
+        cp, ep = corr.ctypes.data_as(A.U32P), en.ctypes.data_as(A.U32P)
+        if _is_device(inp):
+            A.call("srcdsp_corr_step_trace", self._h, _ptr(inp), n, C.byref(found), C.byref(idx), cp, ep,
+                   C.byref(cnt), _stream(inp))
+        else:
+            x = _host(inp, "ci16")
+            A.call("srcdsp_corr_step_host_trace", self._h, _ptr(x), n, C.byref(found), C.byref(idx), cp, ep,
+                   C.byref(cnt))
+        k = cnt.value
+        return bool(found.value), idx.value, corr[:k], en[:k]
+
     def prime(self, inp):
         """Not a reference method: leave the state step() would
         leave after streaming `inp` with no detection test -- seeds a time

@@ -357,3 +357,52 @@ int main() {
         assert r.returncode == 7 and "ShardedDnsamplingFir::step" in r.stdout, (r.returncode, r.stdout, r.stderr)
     else:
         assert r.returncode == 9 and "buffer shapes do not match the call" in r.stderr, (r.returncode, r.stderr)
+
+
+def _corr_debug_golden():
+    import json
+    g = os.path.join(ROOT, "tests", "golden")
+    with open(os.path.join(g, "corr_debug.json")) as f:
+        return json.load(f), np.load(os.path.join(g, "corr_debug.npz"))
+
+
+def test_dropin_corr_debug_files_compile(tmp_path):
+    """CREATE_DEBUG_FILES: tests/cpp/corr_debug_main.cpp compiles against the
+    drop-in with the macro (the reference's move-only object included)."""
+    for n, s_ in ((32, 4), (1024, 1)):
+        r = subprocess.run(["g++", "-std=c++14", "-Wall", "-DCREATE_DEBUG_FILES", f"-DCORR_N={n}", f"-DCORR_S={s_}",
+                            "-I", INC, "-I", "/opt/rocm/include", "-D__HIP_PLATFORM_AMD__", "-fsyntax-only",
+                            os.path.join(ROOT, "tests", "cpp", "corr_debug_main.cpp")], capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key", [c["key"] for c in _corr_debug_golden()[0]["cases"]])
+def test_dropin_corr_debug_files_match_reference(tmp_path, key):
+    """The reference built with CREATE_DEBUG_FILES writes sqrt(energy),
+    sqrt(corr) and 2.5 sqrt(energy) for every processed sample
+    (correlators.h:253-257).  The same program compiled against the drop-in
+    with the macro (step() through srcdsp_corr_step_host_trace) writes the
+    same three files byte for byte, and the same detections
+    (tests/golden/corr_debug.*, made from the reference by gen_corr_debug.py)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    man, arr = _corr_debug_golden()
+    case = [c for c in man["cases"] if c["key"] == key][0]
+    exe = str(tmp_path / "corr_debug_main")
+    r = subprocess.run(["g++", "-std=c++14", "-O2", "-DCREATE_DEBUG_FILES", f"-DCORR_N={case['N']}",
+                        f"-DCORR_S={case['S']}", "-D__HIP_PLATFORM_AMD__", "-I", INC, "-I", "/opt/rocm/include",
+                        os.path.join(ROOT, "tests", "cpp", "corr_debug_main.cpp"), "-o", exe, "-L", LIBDIR,
+                        "-lsrcdsp_hip", f"-Wl,-rpath,{LIBDIR}", "-Wl,-rpath,/opt/rocm/lib"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    run = tmp_path / "run"
+    run.mkdir()
+    (run / "in.bin").write_bytes(arr[key + "_in"].tobytes())
+    r = subprocess.run([exe, "in.bin", "steps.txt"], cwd=str(run), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert (run / "steps.txt").read_bytes() == arr[key + "_steps.txt"].tobytes()
+    for name in man["files"]:
+        got, want = (run / name).read_bytes(), arr[key + "_" + name].tobytes()
+        assert got.count(b"\n") == case["debug_lines"] and got == want, name
