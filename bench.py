@@ -7,10 +7,11 @@ synthetic samples, one step() per timed step (one kernel launch), FMA float
 contract.  With --gpus N (launched by torch.distributed.run) every rank owns
 the same work as N = 1 -- one 2^28-sample channel of its own -- so the N = 1,
 2, 4, 8 values form one weak-scaling series (no collective in the timed
-region).  Beside it, in the same line, `configs2_share` measures configs[2]'s
-layout: 8 channels of 2^28 per GPU (64 over 8 GPUs), one batched step per
-rank, at every N (so that series is weak scaling too), and the RCCL gather of
-every channel's decimated output to rank 0 (32 GiB at N = 8), timed apart.
+region).  Beside it, in the same line at N > 1 (at N = 1 with --share),
+`configs2_share` measures configs[2]'s layout: 8 channels of 2^28 per GPU (64
+over 8 GPUs), one batched step per rank (weak scaling too), and the RCCL
+gather of every channel's decimated output to rank 0 (32 GiB at N = 8), timed
+apart.
 --channels-per-gpu C makes C channels per GPU the main series instead.
 
 Other workloads (--workload): mixdecim (config 4, mixer -> fixed-point
@@ -58,7 +59,10 @@ def parse():
     # per GPU), plus the configs[2] per-GPU share (8 channels) beside it; see
     # channel_layout() and share_layout()
     p.add_argument("--channels-per-gpu", type=int, default=None)
-    p.add_argument("--no-share", action="store_true", help="skip the configs[2] per-GPU share measurement")
+    p.add_argument("--no-share", action="store_true", help="skip the configs[2] per-GPU share measurement (N > 1)")
+    p.add_argument("--share", action="store_true",
+                   help="measure the configs[2] per-GPU share at N = 1 too (default: N > 1 only, so the N = 1 "
+                        "command's kernel trace holds the headline's launches alone)")
     p.add_argument("--fp", default="fma", choices=["fma", "strict"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=1 << 27, help="samples timed on the reference CPU path")
@@ -135,10 +139,14 @@ def channel_layout(args, world: int, L: int | None = None) -> dict:
 
 def share_layout(args, world: int, L: int | None = None) -> dict | None:
     """configs[2]'s per-GPU share measured beside the main series: 8 channels
-    of 2^28 per GPU at every N (64 in all at N = 8), and the gather of every
-    channel's decimated output to rank 0.  None when not measured (other
-    workloads, an explicit --channels-per-gpu, --no-share)."""
+    of 2^28 per GPU (64 in all at N = 8), and the gather of every channel's
+    decimated output to rank 0.  Measured at N > 1 (and at N = 1 with
+    --share: the driver's N = 1 command then profiles the headline's launches
+    alone); None when not measured (other workloads, an explicit
+    --channels-per-gpu, --no-share)."""
     if args.workload != "decim" or args.channels_per_gpu is not None or getattr(args, "no_share", False):
+        return None
+    if world == 1 and not getattr(args, "share", False):
         return None
     if L is None:
         L = args.samples if args.samples is not None else (1 << 28)

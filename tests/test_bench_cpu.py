@@ -61,9 +61,10 @@ def test_channel_layout_matches_baseline_configs():
     """The main series holds the same per-GPU work at every N: one 2^28
     channel per GPU (configs[1] at N = 1), so SCALE's 1/2/4/8 values are weak
     scaling on one layout.  configs[2]'s share (8 x 2^28 per GPU, 64 over 8
-    GPUs, 32 GiB gather at N = 8) is measured beside it at every N, and only
-    N = 8 is labelled configs[2]."""
-    a = types.SimpleNamespace(workload="decim", samples=None, channels_per_gpu=None, no_share=False)
+    GPUs, 32 GiB gather at N = 8) is measured beside it at N > 1 (N = 1 with
+    --share), and only N = 8 is labelled configs[2] (VERDICT r4 item 6,
+    ADVICE r4)."""
+    a = types.SimpleNamespace(workload="decim", samples=None, channels_per_gpu=None, no_share=False, share=False)
     one = bench.channel_layout(a, 1)
     assert one == {"channels_per_gpu": 1, "channels_total": 1, "samples_per_channel": 1 << 28,
                    "baseline_config": "configs[1]"}
@@ -73,7 +74,9 @@ def test_channel_layout_matches_baseline_configs():
         assert lay["baseline_config"] == f"configs[1] on each of {n} GPUs ({n} independent channels)"
     labels = {1: "configs[2] per-GPU layout (8 of 64 channels)", 2: "configs[2] per-GPU layout (16 of 64 channels)",
               4: "configs[2] per-GPU layout (32 of 64 channels)", 8: "configs[2]"}
+    assert bench.share_layout(a, 1) is None  # N = 1: the headline's launches alone unless --share
     for n, want in labels.items():
+        a.share = n == 1
         sh = bench.share_layout(a, n)
         assert sh["channels_per_gpu"] == 8 and sh["channels_total"] == 8 * n and sh["baseline_config"] == want
         assert sh["gather_bytes"] == (8 * n * (1 << 26) * 8 if n > 1 else 0)
@@ -84,7 +87,7 @@ def test_channel_layout_matches_baseline_configs():
     assert bench.share_layout(a, 8) is None
     a.channels_per_gpu = 3
     assert bench.channel_layout(a, 2)["baseline_config"] == "custom"
-    c = types.SimpleNamespace(workload="corr", samples=1 << 26, channels_per_gpu=None, no_share=False)
+    c = types.SimpleNamespace(workload="corr", samples=1 << 26, channels_per_gpu=None, no_share=False, share=True)
     assert bench.channel_layout(c, 8)["channels_per_gpu"] == 1 and bench.channel_layout(c, 8)["baseline_config"] is None
     assert bench.share_layout(c, 8) is None
 
