@@ -102,14 +102,15 @@ def test_sharded_decim_ndev_on_one_gpu(built, tmp_path, ndev, C, root):
     assert got[203] == want  # caller streams ordered by waitFor / signal, no synchronize()
     q, rem = divmod(C, ndev)
     transfers = [l for l in r.stderr.splitlines() if l.startswith("rccl_stub:")]
+    # three contiguous gathers (records 200, 202 and 203) and one strided (201)
     if rem == 0:
-        # ncclGather for both contiguous gathers (each rank incl. the root) and,
+        # ncclGather for every contiguous gather (each rank incl. the root) and,
         # for the strided one, one Send/Recv per non-root row
-        assert len(transfers) == 2 * ndev + (C - q)
+        assert len(transfers) == 3 * ndev + (C - q)
     else:
         nonroot_ranks = sum(1 for k in range(ndev) if k != root and q + (k < rem) > 0)
         nonroot_rows = C - (q + (root < rem))
-        assert len(transfers) == 2 * nonroot_ranks + nonroot_rows
+        assert len(transfers) == 3 * nonroot_ranks + nonroot_rows
 
 
 def test_shared_devices_refused_by_the_product(S, monkeypatch):
