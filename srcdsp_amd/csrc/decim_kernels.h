@@ -1451,12 +1451,22 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
         const int nw = (SEQ1 || SEQR) ? (int)Pe : SEQT ? 2 * (int)Pe : (TAB2 ? 2 : 1) * (int)N;
         // SEQR: entry j is the sample j - HS (mod Pe) of every tile's staging
         const unsigned rot = SEQR ? (unsigned)((long)Pe - (long)HS % (long)Pe) % Pe : 0u;
+        // SEQT: entry i holds the phase of sample i + rot, (phi0 + (i + rot) fr)
+        // mod N -- periodic in Pe, so i + rot needs no reduction; one 64-bit
+        // modulo per lane, then a step of BLOCK entries is one add and one
+        // conditional subtract (a modulo per entry was ~100 VALU: ~8 per wave
+        // tile of config 4 over a workgroup's tiles)
+        unsigned kseq = 0, kstep = 0;
+        if constexpr (SEQT) {
+            kseq = (unsigned)(((unsigned long)a.mix_phase0 + (unsigned long)(t + rot) * fr) % N);
+            kstep = (unsigned)(((unsigned long)BLOCK * fr) % N);
+        }
         for (int i = t; i < nw; i += BLOCK) {
             unsigned k;
             if constexpr (SEQT) {
-                unsigned m = (unsigned)i < Pe ? (unsigned)i : (unsigned)i - Pe;
-                if constexpr (SEQR) m = (m + rot) % Pe;
-                k = (unsigned)(((unsigned long)a.mix_phase0 + (unsigned long)m * fr) % N);
+                k = kseq;
+                kseq += kstep;
+                kseq = kseq >= N ? kseq - N : kseq;
             } else {
                 k = (unsigned)i < N ? (unsigned)i : (unsigned)i - N;
             }
