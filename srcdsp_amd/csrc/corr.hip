@@ -306,8 +306,8 @@ __global__ __launch_bounds__(kCBlock, SRCDSP_CORR_MINW) void corr_scan_s1(const 
     if ((long)best0 < i0) return;  // a hit before this tile is already known (block-uniform)
     // taps front-padded with NP - N zero taps (NP = 16 ceil(N/16), as corr_eval_dot2)
     const int pad = NP - N;
-    // tile sample l (input word i0 - (NP - 1) + l, l = 0 .. TO + NP - 2) -> LDS word lw(l)
-    auto lw = [&](int l) { int lp = l + 1; return lp + 4 * (lp / kCR); };
+    // tile sample l (input word i0 - (NP - 1) + l, l = 0 .. TO + NP - 2) -> LDS word
+    // lp + 4 (lp / 16), lp = l + 1: chunks of 16 samples + 4 pad words
     // Staging by 16-B granules: LDS chunk c (20 words, the last 4 padding)
     // holds tile samples 16c - 1 .. 16c + 14, i.e. input words j0 + 16c + 4q +
     // (0..3), j0 = i0 - NP: 16-aligned, so an aligned input is read with one
@@ -360,7 +360,9 @@ __global__ __launch_bounds__(kCBlock, SRCDSP_CORR_MINW) void corr_scan_s1(const 
             uint32_t sg = 0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const uint4 v = xs4[5 * g + q];
+                typedef uint32_t u4v_t __attribute__((ext_vector_type(4)));
+                u4v_t v = *(const u4v_t *)&xs4[5 * g + q];
+                asm volatile("" : "+v"(v));  // one ds_read_b128 (not 4-B pieces, 4-way conflicting at the 80-B stride)
                 sg += sq(v.x) + sq(v.y) + sq(v.z) + sq(v.w);
             }
             csum[g] = sg;
@@ -370,42 +372,47 @@ __global__ __launch_bounds__(kCBlock, SRCDSP_CORR_MINW) void corr_scan_s1(const 
         for (int g = 0; g < NCk; ++g) eu += csum[t + g];
         e0 = (int32_t)eu;
     }
-    uint32_t A[kCR + 15], B[kCR + 15];
-#pragma unroll
-    for (int j = 0; j < kCR - 1; ++j) B[16 + j] = xs[lw(lb + j)];
+    // Each 16-tap chunk reads its whole 31-word window from LDS (LDS chunks
+    // c0 = t + m0/16 and c0 + 1: 8 ds_read_b128, words j = -1 .. 30 of the
+    // lane window) instead of carrying the previous chunk's 15 words in
+    // registers: the carried words came back from the compiler's early reads
+    // through 15 v_mov per 32 taps, the extra reads cost LDS slots only.
     ConstPtr<uint32_t> tp = const_view<uint32_t>(ptaps);
-    auto chunk = [&](int m0, uint32_t(&cur)[kCR + 15], const uint32_t(&prev)[kCR + 15]) {
+    auto chunk = [&](int m0) {
         asm volatile("" : "+s"(tp));
         uint32_t pw[32];
 #pragma unroll
         for (int k = 0; k < 32; ++k) pw[k] = tp[2 * m0 + k];
-        const uint4 *src = (const uint4 *)xs + 5 * (t + 1 + (m0 >> 4));
+        const uint4 *src = (const uint4 *)xs + 5 * (t + (m0 >> 4));
+        uint32_t W[32];  // W[j + 1] = window word j
+        typedef uint32_t u4v_t __attribute__((ext_vector_type(4)));
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const uint4 q = src[g];
-            cur[kCR - 1 + 4 * g + 0] = q.x;
-            cur[kCR - 1 + 4 * g + 1] = q.y;
-            cur[kCR - 1 + 4 * g + 2] = q.z;
-            cur[kCR - 1 + 4 * g + 3] = q.w;
+        for (int g = 0; g < 8; ++g) {
+            // chunk c0 granules 0..3, chunk c0 + 1 granules 0..3; each a whole
+            // ds_read_b128 (W[0] is unused: left alone the compiler reads chunk
+            // c0 as 4-B pieces, which the 80-B lane stride does not spread)
+            u4v_t q = *(const u4v_t *)(src + (g < 4 ? g : g + 1));
+            asm volatile("" : "+v"(q));
+            W[4 * g + 0] = q.x;
+            W[4 * g + 1] = q.y;
+            W[4 * g + 2] = q.z;
+            W[4 * g + 3] = q.w;
         }
-        auto word = [&](int j) { return j < kCR - 1 ? prev[16 + j] : cur[j]; };
 #pragma unroll
         for (int mm = 0; mm < 16; ++mm) {
             const uint32_t p0 = pw[2 * mm], p1 = pw[2 * mm + 1];
 #pragma unroll
             for (int r = 0; r < kCR; ++r) {
-                const short2_t x = __builtin_bit_cast(short2_t, word(mm + r));
+                const short2_t x = __builtin_bit_cast(short2_t, W[mm + r + 1]);
                 ar[r] = __builtin_amdgcn_sdot2(x, __builtin_bit_cast(short2_t, p0), ar[r], false);
                 ai[r] = __builtin_amdgcn_sdot2(x, __builtin_bit_cast(short2_t, p1), ai[r], false);
             }
         }
     };
     bool dead = false;
-    int m0 = 0;
-    for (int it = 0; m0 + 32 <= NP; m0 += 32, ++it) {
-        chunk(m0, A, B);
-        chunk(m0 + 16, B, A);
-        if ((it & 7) == 7) {  // every 256 taps: has a hit before this tile been found?
+    for (int m0 = 0, it = 0; m0 < NP; m0 += 16, ++it) {  // NP % 16 == 0
+        chunk(m0);
+        if ((it & 15) == 15) {  // every 256 taps: has a hit before this tile been found?
             const unsigned bb = __builtin_amdgcn_readfirstlane(load_best(best));
             if ((long)bb < i0) {
                 dead = true;
@@ -413,7 +420,6 @@ __global__ __launch_bounds__(kCBlock, SRCDSP_CORR_MINW) void corr_scan_s1(const 
             }
         }
     }
-    if (!dead && m0 < NP) chunk(m0, A, B);
     // the two outputs before the tile (for the test at its first two indices)
     if (t < 64) {
         uint32_t ex_c[2] = {c_prev0, c_prev1}, ex_e = e_prev0;
@@ -454,30 +460,37 @@ __global__ __launch_bounds__(kCBlock, SRCDSP_CORR_MINW) void corr_scan_s1(const 
     // and 1 (which need the previous lane's last values) wait for the barrier,
     // and three values per lane live across it instead of 32 (at 5 waves per
     // SIMD the 32 spilled to scratch: 2.25 x the algorithmic HBM bytes)
+    // LDS words of the sliding energy, from per-lane bases (no per-output
+    // index arithmetic): the sample entering output r's window is tile sample
+    // lb + r + NP - 1, word 20 (t + NP/16) + r; the one leaving is tile sample
+    // lb + r - 1 + pad, word 20 t + q + 4 (q >> 4) with q = r + pad (uniform)
+    const uint32_t *xn_base = xs + 20 * (t + NP / 16), *xo_base = xs + 20 * t;
+    auto xo_word = [&](int q) { return xo_base[q + 4 * (q >> 4)]; };
     uint32_t e = (uint32_t)e0;  // the direct sum ran over NP window words, the first pad before the real window
-    for (int q = 0; q < pad; ++q) {
-        const short2_t a = __builtin_bit_cast(short2_t, xs[lw(lb + q)]);
+    for (int q = 0; q < pad; ++q) {  // tile samples lb .. lb + pad - 1 (q + 1 <= 15: one LDS chunk)
+        const short2_t a = __builtin_bit_cast(short2_t, xo_base[q + 1]);
         e -= (uint32_t)__builtin_amdgcn_sdot2(a, a, 0, false);
     }
+    // outputs of this lane inside the call: r < nrem (int compares, no 64-bit index per output)
+    const int nrem = (int)std::min<long>(kCR, n - (i0 + lb));
     uint32_t c_0 = 0, c_1 = 0, e_0 = 0;  // outputs 0 and 1, for the tests after the barrier
     uint32_t cm2 = 0, cm1 = 0, em1 = 0;  // the two outputs before r, the energy before r
-    long hit = -1;                       // first hit among outputs 2..15
+    int hit = -1;                        // first hit among outputs 2..15 (lane-relative)
 #pragma unroll
     for (int r = 0; r < kCR; ++r) {
         if (r > 0) {  // E_i = E_{i-1} + |x_i|^2 - |x_{i-N}|^2
-            const uint32_t xn = xs[lw(lb + r + NP - 1)], xo = xs[lw(lb + r - 1 + pad)];
+            const uint32_t xn = xn_base[r], xo = xo_word(r + pad);
             const short2_t a = __builtin_bit_cast(short2_t, xn), b = __builtin_bit_cast(short2_t, xo);
             e += (uint32_t)__builtin_amdgcn_sdot2(a, a, 0, false) - (uint32_t)__builtin_amdgcn_sdot2(b, b, 0, false);
         }
         const uint32_t c = corr_value(ar[r], ai[r], cs), ev = e >> ((unsigned)((int)cs / 2) & 31u);
-        const long i = i0 + lb + r;
         if (r == 0) {
             c_0 = c;
             e_0 = ev;
         } else if (r == 1) {
             c_1 = c;
-        } else if (!dead && hit < 0 && i < n && corr_hit(cm2, cm1, c, em1)) {
-            hit = i;
+        } else if (!dead && hit < 0 && r < nrem && corr_hit(cm2, cm1, c, em1)) {
+            hit = r;
         }
         cm2 = cm1;
         cm1 = c;
@@ -490,10 +503,9 @@ __global__ __launch_bounds__(kCBlock, SRCDSP_CORR_MINW) void corr_scan_s1(const 
     __syncthreads();
     if (dead_any) return;  // outputs past a known hit: nothing to record
     const uint32_t pc1 = prev_c[t][0], pc2 = prev_c[t][1], pe1 = prev_e[t];
-    const long i = i0 + lb;
-    if (i + 1 < n && corr_hit(pc1, c_0, c_1, e_0)) hit = i + 1;
-    if (i < n && corr_hit(pc2, pc1, c_0, pe1)) hit = i;
-    if (hit >= 0) atomicMin(best, (unsigned)hit);
+    if (1 < nrem && corr_hit(pc1, c_0, c_1, e_0)) hit = 1;
+    if (0 < nrem && corr_hit(pc2, pc1, c_0, pe1)) hit = 0;
+    if (hit >= 0) atomicMin(best, (unsigned)(i0 + lb + hit));
 }
 
 __global__ void corr_detect(const uint32_t *__restrict__ corr, const uint32_t *__restrict__ en, long i_begin,
