@@ -42,6 +42,25 @@ def decim_all(make, x: np.ndarray, M: int, lead: int, out: np.ndarray, win_out: 
     return out
 
 
+def up_all(make, x: np.ndarray, L: int, lead: int, out: np.ndarray, win_in: int = 1 << 18) -> np.ndarray:
+    """Fill out[:] with the interpolator's L * len(x) outputs (fresh state):
+    window [j0, j1) of inputs starts `lead` inputs early (lead >= the ring's
+    taps / L inputs, upsampling_filters.h:166-184) and keeps outputs from
+    L * j0 on."""
+    n = len(x)
+    assert len(out) == L * n
+
+    def job(j0):
+        j1 = min(n, j0 + win_in)
+        lo = max(0, j0 - lead)
+        r = make().step(x[lo:j1])
+        out[L * j0:L * j1] = r[L * (j0 - lo):]
+
+    with cf.ThreadPoolExecutor(WORKERS) as ex:
+        list(ex.map(job, range(0, n, win_in)))
+    return out
+
+
 def first_bad(got: np.ndarray, want: np.ndarray):
     """Index of the first differing output (byte compare), or None."""
     g = np.ascontiguousarray(got).view(np.uint8).reshape(len(got), -1)

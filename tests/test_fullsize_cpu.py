@@ -47,3 +47,20 @@ def test_corr_first_equals_single_call(O, where):
         assert np.array_equal(bits, one.bit_samples())
         s1 = one.status()
         assert all(s1[k] == st[k] for k in ("energy", "corr"))
+
+
+def test_fir_and_up_windows_equal_single_call(O):
+    """The window runs behind the fir / up whole-output GPU tests equal one call."""
+    from srcdsp_amd.design import hamming_sinc, q14
+    o = O["fma"]
+    rng = np.random.default_rng(3)
+    x = rng.integers(-2048, 2048, size=150000).astype(np.float32)
+    c = hamming_sinc(31, 0.2)
+    want = o.fir(1, c).step(x)
+    got = F.decim_all(lambda: o.fir(1, c), x, 1, 32, np.empty_like(want), win_out=7000)
+    assert F.first_bad(got, want) is None
+    xu = o.gen_ci16(5, 0, 0, 70000)
+    cu = q14(hamming_sinc(128, 0.12) * 4)
+    want = o.up(0, 4, cu).step(xu)
+    got = F.up_all(lambda: o.up(0, 4, cu), xu, 4, 40, np.empty_like(want), win_in=6000)
+    assert F.first_bad(got, want) is None

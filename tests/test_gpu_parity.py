@@ -757,34 +757,34 @@ def test_mixdecim_beyond_2p31_samples(S, O):
     torch.cuda.empty_cache()
 
 
-def test_fir_and_up_bench_size_properties(S, O):
-    """The fir and up bench workloads at their full sizes (2^28 float samples
-    through the 31-tap FilterFir<float,cf32,float,float>; 2^26 ci16 inputs
-    through the 128-tap x4 interpolator): output windows against the reference
-    run on the same input windows, started early enough to fill the history."""
+def test_fir_and_up_bench_whole_output(S, O):
+    """The fir and up bench workloads at their full sizes: EVERY output of the
+    31-tap FilterFir<float,cf32,float,float> over 2^28 float samples, and of
+    the 128-tap x4 interpolator over 2^26 complex<int16_t> inputs (2^28
+    outputs), against the oracle in parallel windows started early enough to
+    fill the history (tests/fullsize.py)."""
     import torch
+    import fullsize as F
     from srcdsp_amd.design import hamming_sinc, q14
-    rng = np.random.default_rng(5)
     L = 1 << 28
     x = torch.randint(-2048, 2048, (L,), device="cuda").float()
     c = hamming_sinc(31, 0.2)
     y = S.FilterFir(c, "float", "complex<float>", "float", "float", fp="fma").step(x)
     torch.cuda.synchronize()
-    for s0 in [0, 17, 8191, L - 64, *map(int, rng.integers(32, L - 64, 8))]:
-        lo = max(0, s0 - 32)
-        r = O["fma"].fir(1, c).step(x[lo:s0 + 64].cpu().numpy())[s0 - lo:]
-        assert np.array_equal(y[s0:s0 + 64].cpu().numpy(), r), s0
-    del x, y
+    xh = x.cpu().numpy()
+    want = F.decim_all(lambda: O["fma"].fir(1, c), xh, 1, 32, np.empty(L, np.complex64))
+    bad = F.first_bad(y.cpu().numpy(), want)
+    assert bad is None, f"fir: first differing output {bad}"
+    del x, y, xh, want
     n = 1 << 26
     xu = torch.empty((n, 2), dtype=torch.int16, device="cuda")
     S.fill_synthetic(xu, "ci16", seed=0x5EED, channel=0, lo=-8192, hi=8191)
     cu = q14(hamming_sinc(128, 0.12) * 4)
     yu = S.FilterUpsamplingFir(cu, 4).step(xu)
     torch.cuda.synchronize()
-    for j0 in [0, 5, 2047, n - 64, *map(int, rng.integers(40, n - 64, 8))]:
-        lo = max(0, j0 - 40)
-        r = O["fma"].up(0, 4, cu).step(xu[lo:j0 + 64].cpu().numpy())[4 * (j0 - lo):]
-        assert np.array_equal(yu[4 * j0:4 * (j0 + 64)].cpu().numpy(), r), j0
+    want = F.up_all(lambda: O["fma"].up(0, 4, cu), xu.cpu().numpy(), 4, 40, np.empty((4 * n, 2), np.int16))
+    bad = F.first_bad(yu.cpu().numpy(), want)
+    assert bad is None, f"up: first differing output {bad}"
     del xu, yu
     torch.cuda.empty_cache()
 
