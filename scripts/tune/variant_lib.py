@@ -14,7 +14,10 @@ scripts/tune/ab_libs.sh (LIBS="<name> new").
            with per-granule index arithmetic (form 4, no rotated form 5) and
            zero-initialised accumulators (a v_mov each) in the compiled-tap loop.
 
-    python scripts/tune/variant_lib.py halflds|r4mix
+  rev:<REV> the product sources of git revision REV, unpatched (e.g. rev:HEAD
+           before a kernel change is committed); built as libsrcdsp_hip_<REV>.so
+
+    python scripts/tune/variant_lib.py halflds|r4mix|rev:<REV>
 """
 from __future__ import annotations
 
@@ -62,13 +65,19 @@ PATCHES = {
 
 def main():
     name = sys.argv[1]
-    out = os.path.join(HERE, "ab", f"libsrcdsp_hip_{name}.so")
+    rev = name[4:] if name.startswith("rev:") else None
+    out = os.path.join(HERE, "ab", f"libsrcdsp_hip_{rev or name}.so")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     with tempfile.TemporaryDirectory() as d:
         src = os.path.join(d, "srcdsp_amd", "csrc")  # csrc includes ../../include/srcdsp_hip.h
-        shutil.copytree(B.CSRC, src)
-        shutil.copytree(os.path.join(ROOT, "include"), os.path.join(d, "include"))
-        for fname, old, new in PATCHES[name]:
+        if rev:
+            tar = subprocess.run(["git", "-C", ROOT, "archive", rev, "srcdsp_amd/csrc", "include"],
+                                 check=True, capture_output=True).stdout
+            subprocess.run(["tar", "-x", "-C", d], input=tar, check=True)
+        else:
+            shutil.copytree(B.CSRC, src)
+            shutil.copytree(os.path.join(ROOT, "include"), os.path.join(d, "include"))
+        for fname, old, new in ([] if rev else PATCHES[name]):
             k = os.path.join(src, fname)
             text = open(k).read()
             assert text.count(old) == 1, f"patch site not found in {fname}"

@@ -153,9 +153,10 @@ int launch_ci16_dot2(DecimLaunch L, int channels, bool mixed, hipStream_t s) {
     // two-word sequence tables: stored twice up to Pe = 2048, once (index
     // wrapped) up to 4096 -- config 4's mixer (N = 4096, f = 0.1: freq word
     // 205, Pe = 4096) takes the latter
-    // the period dividing the tile's input span (16 BLOCK samples): the rotated
-    // table, no index arithmetic per granule (config 4: Pe = 4096 | 8192)
-    if constexpr (BLOCK == 512)
+    // the period dividing the tile's input span (16 BLOCK samples): the lane's
+    // table words in registers (config 4: Pe = 4096 | 8192); not for runtime
+    // taps at M = 2, whose 16 more VGPRs would spill past the 128 of MINW = 4
+    if constexpr (BLOCK == 512 && !(NT == 0 && MD == 2))
         if ((16u * BLOCK) % pe == 0) return launch_ci16_dot2_shape<NT, BLOCK, 5, MD>(L, channels, mixed, s);
     if (pe <= (unsigned)kSeq2Max) return launch_ci16_dot2_shape<NT, BLOCK, 3, MD>(L, channels, mixed, s);
     return launch_ci16_dot2_shape<NT, BLOCK, 4, MD>(L, channels, mixed, s);

@@ -1384,14 +1384,15 @@ __global__ __launch_bounds__(kDtBlock) void decim_tile(DecimLaunch a) {
 //  4 (two-word sequence table stored once, Pe <= kSeq2Off): as 3 with each
 //    table held once (2 Pe words: the LDS of form 2's doubled one-word table),
 //    the granule's index m + lo (< 2 Pe) wrapped by one subtract and one min.
-//  5 (two-word sequence table stored once and ROTATED, Pe | SPT, 512 lanes):
-//    when the period divides the tile's input span (config 4: N = 4096, any
-//    frequency, Pe a power of two <= 4096), every tile's first staged sample
-//    has the same table index m0 = -HS mod Pe, so the tables are stored
-//    rotated by m0 and staged granule g = t + i BLOCK of every tile reads
-//    index (4 t + 4 i BLOCK) mod Pe = (4 t mod Pe) + (i odd ? 2048 mod Pe : 0)
-//    < Pe: two per-lane base addresses made once, no index arithmetic per
-//    granule (form 4 spends 4 VALU per granule on it).
+//  5 (two-word sequence in REGISTERS, Pe | SPT, 512 lanes): when the period
+//    divides the tile's input span (config 4: N = 4096, any frequency, Pe a
+//    power of two <= 4096), staged granule g = t + i BLOCK of every tile after
+//    the first holds samples (4 t + (i odd ? 2048 : 0) + j - HS) mod Pe, so a
+//    lane needs only 2 x 4 (A, B) word pairs: made once from the global LUT
+//    into 16 VGPRs, no LDS table, no table fill, no table read per granule
+//    (round 5's first form stored the table rotated by -HS in LDS and read
+//    8 ds_read_b128 per lane-tile; form 4 spends 4 VALU per granule on the
+//    index).  Tile 0 and the history read the global LUT per sample.
 // Products via VOP3 dot2 and the pair clamp above.
 constexpr int kSeq2Off = 4096, kSeq2Max = kSeq2Off / 2;
 template <int NT, int BLOCK, bool MIX, int MINW, int TABM = 0, int MD = 4>
@@ -1414,7 +1415,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     constexpr int NC0 = ceildiv(PG, 2);
     constexpr int NC = NC0 + ((4 - NC0 % 8) + 8) % 8;  // slots per plane row, = 4 (mod 8)
     constexpr int LSLOTS = 4 * NC;
-    constexpr int TABMAX = MIX ? (TABM ? 8192 : 4096) : 1;
+    constexpr int TABMAX = (MIX && !SEQR) ? (TABM ? 8192 : 4096) : 1;  // SEQR: the lane's words in registers
     static_assert(HSC % 16 == 0 && 2 * (JC - 1) <= HSC, "halo geometry");
     static_assert(BLOCK % 16 == 0, "column-major plane layout");
     // tap pairs (RT: padded with zero pairs to whole 4-pair steps), halo
@@ -1446,19 +1447,41 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     const long t_end = t_begin + per + (b < rem ? 1 : 0);
 
     const unsigned Pe = SEQT ? a.mix_pe : 1u;
-    if constexpr (MIX) {
+    // SEQR: every tile's staged granule t + i BLOCK reads the same 4 samples'
+    // table words -- index (4 t + (i odd ? 2048 : 0) + j - HS) mod Pe -- so the
+    // lane keeps its two granules' words (A = (lr, -li), B = (li, lr)) in 16
+    // registers, made once from the global LUT (one 64-bit modulo per parity,
+    // then a phase step per sample), and no table lives in LDS
+    uint32_t rA[2][4] = {}, rB[2][4] = {};
+    if constexpr (MIX && SEQR) {
         const int16_t *tab = a.mix_table;
-        const int nw = (SEQ1 || SEQR) ? (int)Pe : SEQT ? 2 * (int)Pe : (TAB2 ? 2 : 1) * (int)N;
-        // SEQR: entry j is the sample j - HS (mod Pe) of every tile's staging
-        const unsigned rot = SEQR ? (unsigned)((long)Pe - (long)HS % (long)Pe) % Pe : 0u;
-        // SEQT: entry i holds the phase of sample i + rot, (phi0 + (i + rot) fr)
-        // mod N -- periodic in Pe, so i + rot needs no reduction; one 64-bit
+        const unsigned hs = (unsigned)((long)HS % (long)Pe);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const unsigned m = (4u * t + (h ? 2048u % Pe : 0u) + Pe - hs) % Pe;  // sample offset of word j = 0
+            unsigned k = (unsigned)(((unsigned long)a.mix_phase0 + (unsigned long)m * fr) % N);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                unsigned ic = k + N / 4;
+                ic = ic >= N ? ic - N : ic;
+                rA[h][j] = ((uint32_t)(uint16_t)tab[ic]) | ((uint32_t)(uint16_t)(-tab[k]) << 16);
+                rB[h][j] = ((uint32_t)(uint16_t)tab[k]) | ((uint32_t)(uint16_t)tab[ic] << 16);
+                k += fr;
+                k = k >= N ? k - N : k;
+            }
+        }
+    }
+    if constexpr (MIX && !SEQR) {
+        const int16_t *tab = a.mix_table;
+        const int nw = SEQ1 ? (int)Pe : SEQT ? 2 * (int)Pe : (TAB2 ? 2 : 1) * (int)N;
+        // SEQT: entry i holds the phase of sample i, (phi0 + i fr) mod N --
+        // periodic in Pe, so i needs no reduction; one 64-bit
         // modulo per lane, then a step of BLOCK entries is one add and one
         // conditional subtract (a modulo per entry was ~100 VALU: ~8 per wave
         // tile of config 4 over a workgroup's tiles)
         unsigned kseq = 0, kstep = 0;
         if constexpr (SEQT) {
-            kseq = (unsigned)(((unsigned long)a.mix_phase0 + (unsigned long)(t + rot) * fr) % N);
+            kseq = (unsigned)(((unsigned long)a.mix_phase0 + (unsigned long)t * fr) % N);
             kstep = (unsigned)(((unsigned long)BLOCK * fr) % N);
         }
         for (int i = t; i < nw; i += BLOCK) {
@@ -1485,7 +1508,13 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     auto phase_add = [&](unsigned base, unsigned k) { return (base + (k % N) * fr) % N; };
     auto mix1 = [&](uint32_t w, unsigned ph) {
         int32_t re, im;
-        if constexpr (SEQ2) {
+        if constexpr (SEQR) {  // no LDS table: ph is the phase itself, the words from the global LUT
+            unsigned ic = ph + N / 4;
+            ic = ic >= N ? ic - N : ic;
+            const int16_t lr = a.mix_table[ic], li = a.mix_table[ph];
+            re = clamp_s14(sdot2(w, ((uint32_t)(uint16_t)lr) | ((uint32_t)(uint16_t)(-li) << 16), 0));
+            im = clamp_s14(sdot2(w, ((uint32_t)(uint16_t)li) | ((uint32_t)(uint16_t)lr << 16), 0));
+        } else if constexpr (SEQ2) {
             re = clamp_s14(sdot2(w, ctab[ph], 0));
             im = clamp_s14(sdot2(w, ctab[kSeq2Off + ph], 0));
         } else {
@@ -1495,7 +1524,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
     };
     // input sample s >= 0 of this call, mixed (any table form)
     auto mix_at = [&](uint32_t w, long s) {
-        if constexpr (SEQR) return mix1(w, (unsigned)((s + HS) % (long)Pe));  // the table is rotated by -HS
+        if constexpr (SEQR) return mix1(w, phase_add(a.mix_phase0, (unsigned)(s % (long)N)));
         else if constexpr (SEQT) return mix1(w, (unsigned)(s % (long)Pe));
         else return mix1(w, phase_add(a.mix_phase0, (unsigned)(s % (long)N)));
     };
@@ -1595,17 +1624,14 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
         *lds_half(g, 0) = make_uint2(clamp_pair_s14(r0, r1), clamp_pair_s14(r2, r3));
         *lds_half(g, 1) = make_uint2(clamp_pair_s14(i0, i1), clamp_pair_s14(i2, i3));
     };
-    // SEQR: byte addresses of the lane's granule in even / odd rounds
-    const unsigned seqr_b0 = SEQR ? 4u * ((4u * t) % Pe) : 0u;
-    const unsigned seqr_b1 = SEQR ? 4u * ((4u * t) % Pe + 2048u % Pe) : 0u;
-    auto put_mixed_seqr = [&](int g, uint4 w, unsigned bytes) {
-        const char *tb = (const char *)ctab;
-        const uint4 A = *(const uint4 *)__builtin_assume_aligned(tb + bytes, 16);
-        const uint4 B = *(const uint4 *)__builtin_assume_aligned(tb + bytes + 4 * kSeq2Off, 16);
-        const int32_t r0 = sdot2_0(w.x, A.x), i0 = sdot2_0(w.x, B.x);
-        const int32_t r1 = sdot2_0(w.y, A.y), i1 = sdot2_0(w.y, B.y);
-        const int32_t r2 = sdot2_0(w.z, A.z), i2 = sdot2_0(w.z, B.z);
-        const int32_t r3 = sdot2_0(w.w, A.w), i3 = sdot2_0(w.w, B.w);
+    // SEQR: the round's parity picks the lane's register words
+    auto put_mixed_seqr = [&](int g, uint4 w, int h) {
+        const uint32_t(&A)[4] = rA[h];
+        const uint32_t(&B)[4] = rB[h];
+        const int32_t r0 = sdot2_0(w.x, A[0]), i0 = sdot2_0(w.x, B[0]);
+        const int32_t r1 = sdot2_0(w.y, A[1]), i1 = sdot2_0(w.y, B[1]);
+        const int32_t r2 = sdot2_0(w.z, A[2]), i2 = sdot2_0(w.z, B[2]);
+        const int32_t r3 = sdot2_0(w.w, A[3]), i3 = sdot2_0(w.w, B[3]);
         *lds_half(g, 0) = make_uint2(clamp_pair_s14(r0, r1), clamp_pair_s14(r2, r3));
         *lds_half(g, 1) = make_uint2(clamp_pair_s14(i0, i1), clamp_pair_s14(i2, i3));
     };
@@ -1663,7 +1689,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void decim_dot2_ci16(DecimLaunch a) {
 #pragma unroll
             for (int i = 0; i < PER; ++i) {
                 const int g = sg(i);
-                if (g >= 0) put_mixed_seqr(g, v[i], (i & 1) ? seqr_b1 : seqr_b0);
+                if (g >= 0) put_mixed_seqr(g, v[i], i & 1);
             }
         } else if (MIX && SEQT && tile != 0) {
             unsigned m = m_tile;  // wave-uniform
