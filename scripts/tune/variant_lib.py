@@ -14,6 +14,11 @@ scripts/tune/ab_libs.sh (LIBS="<name> new").
            with per-granule index arithmetic (form 4, no rotated form 5) and
            zero-initialised accumulators (a v_mov each) in the compiled-tap loop.
 
+  r8       the headline at 8 outputs per lane (32-sample lane chunks: 160-sample
+           windows for 8 outputs, 44 % fewer LDS window reads per output) in
+           256-lane workgroups (the same 8192-sample tiles and LDS image), 2
+           waves per SIMD (the wider window and the doubled per-lane prefetch
+           need up to 256 VGPRs)
   rev:<REV> the product sources of git revision REV, unpatched (e.g. rev:HEAD
            before a kernel change is committed); built as libsrcdsp_hip_<REV>.so
 
@@ -21,6 +26,7 @@ scripts/tune/ab_libs.sh (LIBS="<name> new").
 """
 from __future__ import annotations
 
+import concurrent.futures as cf
 import glob
 import os
 import shutil
@@ -47,6 +53,56 @@ PATCHES = {
                     asm volatile("" : "=v"(g0.x), "=v"(g0.y), "=v"(g0.z), "=v"(g0.w));
                     asm volatile("" : "=v"(g1.x), "=v"(g1.y), "=v"(g1.z), "=v"(g1.w));
                 }""")],
+    "r8": [("decim_kernels.h", """    static_assert((M * R) % 4 == 0 && M * R <= 16, "a lane chunk is 4, 8, 12 or 16 input samples");""",
+            """    static_assert((M * R) % 4 == 0 && M * R <= 32, "a lane chunk is 4 to 32 input samples");"""),
+           ("cf32_launch.h", """template <int NT, int M = 4>
+int launch_cf32(DecimLaunch L, int channels, bool fma, hipStream_t s) {
+    constexpr int R = cf32_r<M>(), TO = kCfBlock * R;""", """template <int NT, int M = 4>
+int launch_cf32(DecimLaunch L, int channels, bool fma, hipStream_t s) {
+    if constexpr (M == 4 && NT != 0) return launch_cf32_r8<NT>(L, channels, fma, s);
+    constexpr int R = cf32_r<M>(), TO = kCfBlock * R;"""),
+           ("cf32_launch.h", """template <int NT, int M = 4>
+int launch_cf32(""", """template <int NT>
+int launch_cf32_r8(DecimLaunch L, int channels, bool fma, hipStream_t s) {
+    constexpr int R = 8, B = 256, TO = B * R;
+    L.ntiles = (L.n_out + TO - 1) / TO;
+    dim3 grid((unsigned)std::min<long>(L.ntiles, kCfGrid), channels);
+    const bool q0 = (L.shift & 31u) == 0;
+    if (fma && q0) hipLaunchKernelGGL((decim_stream_cf32<NT, R, B, true, 2, true, 4>), grid, dim3(B), 0, s, L);
+    else if (fma) hipLaunchKernelGGL((decim_stream_cf32<NT, R, B, true, 2, false, 4>), grid, dim3(B), 0, s, L);
+    else if (q0) hipLaunchKernelGGL((decim_stream_cf32<NT, R, B, false, 2, true, 4>), grid, dim3(B), 0, s, L);
+    else hipLaunchKernelGGL((decim_stream_cf32<NT, R, B, false, 2, false, 4>), grid, dim3(B), 0, s, L);
+    return SRCDSP_OK;
+}
+template <int NT, int M = 4>
+int launch_cf32(""")
+           # the compiled-tap window in EH + 3 rotating group slots (as the
+           # runtime-tap path): the flat 4 (NQ + GPC) array is not promoted to
+           # registers at GPC = 8
+           , ("decim_kernels.h", """            float2 X[4 * (NQC + GPC)];
+            auto load_group = [&](int e) {
+                const float4 g0 = rd(Bt + 2 * e + floordiv(2 * e, PR));
+                const float4 g1 = rd(Bt + 2 * e + 1 + floordiv(2 * e + 1, PR));
+                X[4 * e + 4 * NQC + 0] = make_float2(g0.x, g0.y);
+                X[4 * e + 4 * NQC + 1] = make_float2(g0.z, g0.w);
+                X[4 * e + 4 * NQC + 2] = make_float2(g1.x, g1.y);
+                X[4 * e + 4 * NQC + 3] = make_float2(g1.z, g1.w);
+            };""", """            constexpr int SL = (M * (R - 1)) / 4 + 3;
+            float2 X[SL][4];
+            auto slot = [](int e) { return ((e % SL) + SL) % SL; };
+            auto load_group = [&](int e) {
+                const float4 g0 = rd(Bt + 2 * e + floordiv(2 * e, PR));
+                const float4 g1 = rd(Bt + 2 * e + 1 + floordiv(2 * e + 1, PR));
+                X[slot(e)][0] = make_float2(g0.x, g0.y);
+                X[slot(e)][1] = make_float2(g0.z, g0.w);
+                X[slot(e)][2] = make_float2(g1.x, g1.y);
+                X[slot(e)][3] = make_float2(g1.z, g1.w);
+            };"""),
+           ("decim_kernels.h", """                auto xs = [&](int r, int p) { return X[M * r - 4 * q - p + 4 * NQC]; };""",
+            """                auto xs = [&](int r, int p) {
+                    const int s = M * r - 4 * q - p;
+                    return X[slot(floordiv(s, 4))][s - 4 * floordiv(s, 4)];
+                };""")],
     "r4mix": [("decim.hip", """    if constexpr (BLOCK == 512)
         if ((16u * BLOCK) % pe == 0) return""", """    if constexpr (false)
         if ((16u * BLOCK) % pe == 0) return"""),
@@ -60,6 +116,14 @@ PATCHES = {
                         yr[r] = sdot2(Dr[OFF + 2 * r], P, z0);
                         yi[r] = sdot2(Di[OFF + 2 * r], P, z1);
                     } else {""")],
+}
+
+
+# extra compiler flags of a variant (the whole library)
+FLAGS = {
+    # the R = 8 tap loop (32 steps x 32 pk_fma) is past the default
+    # pragma-unroll threshold: not unrolled, its window goes to scratch
+    "r8": ["-mllvm", "-pragma-unroll-threshold=1000000"],
 }
 
 
@@ -83,11 +147,14 @@ def main():
             assert text.count(old) == 1, f"patch site not found in {fname}"
             open(k, "w").write(text.replace(old, new))
         hipcc = B._hipcc()
-        objs = []
-        for s in sorted(glob.glob(os.path.join(src, "*.hip"))):
-            o = s + ".o"
-            subprocess.run([hipcc, *B.CXXFLAGS, "-c", s, "-o", o], check=True)
-            objs.append(o)
+        srcs = sorted(glob.glob(os.path.join(src, "*.hip")))
+        objs = [s + ".o" for s in srcs]
+
+        def cc(s):
+            subprocess.run([hipcc, *B.CXXFLAGS, *FLAGS.get(name, []), "-c", s, "-o", s + ".o"], check=True)
+
+        with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+            list(ex.map(cc, srcs))
         subprocess.run([hipcc, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", out, *objs, "-ldl",
                         f"-Wl,-rpath,{B.ROCM_LIB}"], check=True)
     print(out)
