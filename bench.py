@@ -43,7 +43,7 @@ VALU_PEAK_TOPS = 39.32  # 256 CUs x 4 SIMD x 16 lanes x 2.4 GHz, one v_dot2 each
 SEED = 0x5EED
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     # The chip's clocks settle only after ~50 back-to-back launches (measured:
@@ -73,7 +73,10 @@ def parse():
     p.add_argument("--dry-run", action="store_true",
                    help="start the ranks, rendezvous over gloo, print each rank's view of the world, exit "
                         "before any GPU call (tests the launcher on a CPU host)")
-    return p.parse_args()
+    p.add_argument("--no-parity", action="store_true",
+                   help="skip the post-timing digest check of the decimated channels")
+    p.add_argument("--digests", default=os.path.join(ROOT, "tests", "golden", "channel_digests.json"))
+    return p.parse_args(argv)
 
 
 def _free_port() -> int:
@@ -182,11 +185,80 @@ def dry_run(args) -> None:
         raise SystemExit(f"bench: rank {rank} sees world {world}/{seen}, --gpus {args.gpus}")
 
 
+class CudaDevice:
+    """Every device call bench.py makes, in one place: torch.cuda on the GPU
+    box.  HostDevice (below) stands in for it in the CPU rehearsal of main()
+    (tests/test_bench_cpu.py), which drives the whole N > 1 path -- timing,
+    parity digests, configs[2] share, gather, line assembly -- on gloo ranks
+    with a host stand-in for the operators."""
+    name = "cuda"
+
+    def __init__(self):
+        import torch
+        self.torch = torch
+
+    def set_device(self, i):
+        self.torch.cuda.set_device(i)
+
+    def device_count(self):
+        return self.torch.cuda.device_count()
+
+    def synchronize(self):
+        self.torch.cuda.synchronize()
+
+    def stream(self):
+        return self.torch.cuda.current_stream()
+
+    def event_pair(self):
+        E = self.torch.cuda.Event
+        return E(enable_timing=True), E(enable_timing=True)
+
+    def empty_cache(self):
+        self.torch.cuda.empty_cache()
+
+
+class _HostEvent:
+    def record(self, stream=None):
+        self.t = time.perf_counter()
+
+    def elapsed_time(self, end):
+        return (end.t - self.t) * 1e3
+
+
+class HostDevice(CudaDevice):
+    """Host stand-in for CudaDevice (CPU rehearsal only: its times are host
+    wall times of the stand-in operators, never a measurement)."""
+    name = "cpu"
+
+    def __init__(self):
+        pass
+
+    def set_device(self, i):
+        pass
+
+    def device_count(self):
+        return 1
+
+    def synchronize(self):
+        pass
+
+    def stream(self):
+        return None
+
+    def event_pair(self):
+        return _HostEvent(), _HostEvent()
+
+    def empty_cache(self):
+        pass
+
+
+DEV = None  # set by main(): CudaDevice() unless a HostDevice is passed in
+
 # "nccl" (= RCCL over xGMI) on a multi-GPU node.  SRCDSP_BENCH_BACKEND=gloo is
 # only for rehearsing the N > 1 code path with several ranks on ONE GPU (the
 # collectives then move host copies); its timings are not scaling numbers.
 BACKEND = os.environ.get("SRCDSP_BENCH_BACKEND", "nccl")
-COLL_DEV = "cuda" if BACKEND == "nccl" else None
+COLL_DEV = "cuda" if BACKEND == "nccl" else None  # device of the collectives' small tensors
 
 
 def dist_setup(args):
@@ -197,22 +269,21 @@ def dist_setup(args):
     if world > 1:
         import torch.distributed as dist
         if BACKEND == "nccl":
-            torch.cuda.set_device(local)
+            DEV.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
-            torch.cuda.set_device(local % torch.cuda.device_count())
+            DEV.set_device(local % DEV.device_count())
             dist.init_process_group("gloo")
     else:
-        torch.cuda.set_device(0)
+        DEV.set_device(0)
     return world, rank, local
 
 
 def barrier(world):
-    import torch
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
-    torch.cuda.synchronize()
+    DEV.synchronize()
 
 
 # ---------------------------------------------------------------- workloads
@@ -235,10 +306,10 @@ class DecimWorkload(Workload):
         from srcdsp_amd.design import hamming_sinc
         self.c = hamming_sinc(127)
         self.L, self.C = L, channels
-        self.x = torch.empty((channels, L), dtype=torch.complex64, device="cuda")
+        self.x = torch.empty((channels, L), dtype=torch.complex64, device=DEV.name)
         for ch in range(channels):
             S.fill_synthetic(self.x[ch], "cf32", seed=SEED, channel=rank * channels + ch)
-        self.y = torch.empty((channels, L // 4), dtype=torch.complex64, device="cuda")
+        self.y = torch.empty((channels, L // 4), dtype=torch.complex64, device=DEV.name)
         self.f = [S.FilterDnsamplingFir(self.c, 4, fp=fp) for _ in range(channels)]
         self.S = S
         self.name = "decim_cf32_m4_t127"
@@ -263,9 +334,9 @@ class MixDecimWorkload(Workload):
     def __init__(self, S, torch, L, channels, rank, fp):
         from srcdsp_amd.design import hamming_sinc, q14
         cq = q14(hamming_sinc(127))
-        self.x = torch.empty((L, 2), dtype=torch.int16, device="cuda")
+        self.x = torch.empty((L, 2), dtype=torch.int16, device=DEV.name)
         S.fill_synthetic(self.x, "ci16", seed=SEED, channel=rank, lo=-8192, hi=8191)
-        self.y = torch.empty((L // 4, 2), dtype=torch.int16, device="cuda")
+        self.y = torch.empty((L // 4, 2), dtype=torch.int16, device=DEV.name)
         m = S.Mixer(4096)
         m.reset(0.1)
         d = S.FilterDnsamplingFir(cq, 4, "complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int32_t")
@@ -321,8 +392,8 @@ class FirWorkload(Workload):
 
     def __init__(self, S, torch, L, channels, rank, fp):
         from srcdsp_amd.design import hamming_sinc
-        self.x = torch.randint(-2048, 2048, (L,), device="cuda").float()
-        self.y = torch.empty(L, dtype=torch.complex64, device="cuda")
+        self.x = torch.randint(-2048, 2048, (L,), device=DEV.name).float()
+        self.y = torch.empty(L, dtype=torch.complex64, device=DEV.name)
         self.f = S.FilterFir(hamming_sinc(31, 0.2), "float", "complex<float>", "float", "float", fp=fp)
         self.name = "fir_f32_t31"
 
@@ -344,9 +415,9 @@ class UpWorkload(Workload):
     def __init__(self, S, torch, L, channels, rank, fp):
         from srcdsp_amd.design import hamming_sinc, q14
         n = L // 4  # keep the output (4n samples) the size of the other workloads' input
-        self.x = torch.empty((n, 2), dtype=torch.int16, device="cuda")
+        self.x = torch.empty((n, 2), dtype=torch.int16, device=DEV.name)
         S.fill_synthetic(self.x, "ci16", seed=SEED, channel=rank, lo=-8192, hi=8191)
-        self.y = torch.empty((4 * n, 2), dtype=torch.int16, device="cuda")
+        self.y = torch.empty((4 * n, 2), dtype=torch.int16, device=DEV.name)
         self.f = S.FilterUpsamplingFir(q14(hamming_sinc(128, 0.12) * 4), 4)
         self.n = n
         self.name = "up_ci16_q14_l4_t128"
@@ -366,9 +437,9 @@ class Ci16DecimWorkload(Workload):
     def __init__(self, S, torch, L, channels, rank, fp):
         from srcdsp_amd.design import hamming_sinc, q14
         cq = q14(hamming_sinc(127))
-        self.x = torch.empty((L, 2), dtype=torch.int16, device="cuda")
+        self.x = torch.empty((L, 2), dtype=torch.int16, device=DEV.name)
         S.fill_synthetic(self.x, "ci16", seed=SEED, channel=rank, lo=-8192, hi=8191)
-        self.y = torch.empty((L // 4, 2), dtype=torch.int16, device="cuda")
+        self.y = torch.empty((L // 4, 2), dtype=torch.int16, device=DEV.name)
         self.d = S.FilterDnsamplingFir(cq, 4, "complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int32_t")
         self.name = "decim_ci16_q14_m4_t127"
 
@@ -404,8 +475,8 @@ class FifoWorkload(Workload):
         rng = np.random.default_rng(rank)
         self.h = rng.integers(-8192, 8192, size=(self.B, 2)).astype(np.int16)
         self.fifo = S.FifoWithTimeTrack(np.dtype(("<i2", 2)), 4 * self.B)
-        self.x = torch.empty((self.B, 2), dtype=torch.int16, device="cuda")
-        self.y = torch.empty((self.B // 4, 2), dtype=torch.int16, device="cuda")
+        self.x = torch.empty((self.B, 2), dtype=torch.int16, device=DEV.name)
+        self.y = torch.empty((self.B // 4, 2), dtype=torch.int16, device=DEV.name)
         self.chain = _mixdecim_chain(S)
         self.name = f"fifo_ring{4 * self.B}_block{self.B}_ci16_to_mixdecim"
         self.n = self.B
@@ -437,7 +508,7 @@ class IqLoadWorkload(Workload):
         tmp = os.environ.get("TMPDIR", "/tmp")
         self.path = os.path.join(tmp, f"srcdsp_bench_iq_{os.getpid()}_{rank}.bin")
         files.saveBinarySamples(rng.integers(-8192, 8192, size=(self.B, 2)).astype(np.int16), self.path)
-        self.y = torch.empty((self.B // 4, 2), dtype=torch.int16, device="cuda")
+        self.y = torch.empty((self.B // 4, 2), dtype=torch.int16, device=DEV.name)
         self.chain = _mixdecim_chain(S)
         self.name = f"iq_capture{self.B}_ci16_to_mixdecim"
         self.n = self.B
@@ -531,58 +602,125 @@ def host_cores():
                f"machine nproc {total}")
 
 
-def cpu_baseline_allcores(args, threads=None):
-    """the reference on all the host cores this GPU's share of the box
-    gives (host_cores()), one independent channel per thread (config 3's layout):
-    each thread owns a FilterDnsamplingFir object from oracle/_ref/strict and
-    steps its own channel; value = all threads' samples / the wall time from the
-    common start to the last thread's end.  ctypes drops the GIL for the calls."""
-    import threading
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import pyoracle
-    from srcdsp_amd.design import hamming_sinc
+def cpu_topology():
+    """The CPUs of this process's affinity mask and one CPU per physical core
+    among them (the lowest-numbered SMT sibling of each (package, core_id),
+    from /sys/devices/system/cpu/cpu*/topology)."""
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        cpus = list(range(os.cpu_count() or 1))
+    first = {}
+    for c in cpus:
+        try:
+            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+            with open(base + "physical_package_id") as f:
+                pkg = int(f.read())
+            with open(base + "core_id") as f:
+                core = int(f.read())
+        except (OSError, ValueError):
+            pkg, core = 0, c
+        first.setdefault((pkg, core), c)
+    return cpus, sorted(first.values())
+
+
+def _ref_decim_lib():
     path = os.path.join(ROOT, "oracle", "_ref", "strict", "libref_decim_old.so")
-    if args.workload != "decim" or not os.path.exists(path):
+    if not os.path.exists(path):
         return None
-    cores_note = f"{threads} threads (caller-set)"
-    if threads is None:
-        threads, cores_note = host_cores()
     lib = C.CDLL(path)
     lib.ref_decim_create.restype = C.c_void_p
     lib.ref_decim_create.argtypes = [C.c_int, C.c_uint, C.c_void_p, C.c_int]
     lib.ref_decim_step_timed.restype = C.c_double
     lib.ref_decim_step_timed.argtypes = [C.c_void_p, C.c_void_p, C.c_long, C.c_void_p]
     lib.ref_decim_destroy.argtypes = [C.c_void_p]
-    # ~2 s of CPU per thread whatever the thread count (bounded host memory)
-    n = min(args.cpu_sample // 2, args.samples // 2, (16 << 26) // threads)  # <= 8 GiB of input in all
-    n -= n % 4
+    return lib
+
+
+def _ref_threads(lib, pins, n, reps):
+    """len(pins) threads, thread i pinned to CPU pins[i] (None: unpinned),
+    each owning a reference FilterDnsamplingFir<cf32,...,4> (oracle/_ref/strict)
+    and channel i of the synthetic workload (n samples, generated by the thread
+    itself), stepping it `reps` times (the stream continues over the same
+    block).  Returns (samples/s over all threads, wall seconds): all threads'
+    samples / the time from the common start to the last thread's end.  ctypes
+    drops the GIL for the calls."""
+    import threading
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    from srcdsp_amd.design import hamming_sinc
     c = hamming_sinc(127)
     o = pyoracle.Oracle(0)
-    xs = [o.gen_cf32(SEED, ch, 0, n) for ch in range(threads)]  # channel ch of the synthetic workload
-    ys = [np.zeros(n // 4, np.complex64) for _ in range(threads)]
-    hs = [lib.ref_decim_create(0, 4, c.ctypes.data, 127) for _ in range(threads)]
-    start = threading.Barrier(threads + 1)
-    ends = [0.0] * threads
+    T = len(pins)
+    start = threading.Barrier(T + 1)
+    ends = [0.0] * T
+    err = []
 
     def run(i):
+        try:
+            if pins[i] is not None:
+                os.sched_setaffinity(0, {pins[i]})  # this thread only (Linux: pid 0 = the calling thread)
+            x = o.gen_cf32(SEED, i, 0, n)
+            y = np.zeros(n // 4, np.complex64)
+            h = lib.ref_decim_create(0, 4, c.ctypes.data, 127)
+        except Exception as e:  # keep the barrier count right
+            err.append(e)
+            start.wait()
+            return
         start.wait()
-        lib.ref_decim_step_timed(hs[i], xs[i].ctypes.data, n, ys[i].ctypes.data)
+        for _ in range(reps):
+            lib.ref_decim_step_timed(h, x.ctypes.data, n, y.ctypes.data)
         ends[i] = time.perf_counter()
+        lib.ref_decim_destroy(h)
 
-    th = [threading.Thread(target=run, args=(i,)) for i in range(threads)]
+    th = [threading.Thread(target=run, args=(i,)) for i in range(T)]
     for t in th:
         t.start()
     start.wait()
     t0 = time.perf_counter()
     for t in th:
         t.join()
+    if err:
+        raise err[0]
     wall = max(ends) - t0
-    for h in hs:
-        lib.ref_decim_destroy(h)
-    return {"value": round(threads * n / wall / 1e6, 3), "unit": "Msamples/s", "cores": threads, "kind": "reference",
-            "sample": f"{threads} threads x {n} samples (channels 0..{threads - 1} of the synthetic workload, one "
-                      f"FilterDnsamplingFir per thread), {wall:.2f} s wall; oracle/_ref/strict/libref_decim_old.so; "
-                      f"host CPU: {_cpu_model()}; {cores_note}"}
+    return T * n * reps / wall, wall
+
+
+def cpu_baseline_allcores(args, threads=None):
+    """the reference on ALL the host's cores, one independent
+    channel per thread (config 3's layout): every hardware thread of the
+    affinity mask (= nproc on the GPU box), and one thread per physical core;
+    beside them the job's CPU share (host_cores(): 16 threads on the MI355X
+    pool).  Each thread is pinned to its CPU and steps its own reference
+    object (oracle/_ref/strict, g++ -O2) over 2^22 samples of its channel 4
+    times (2^24 samples per thread, bounded host memory: 128 MiB of samples per
+    thread).  `threads` (tests) replaces the three runs by one unpinned run of
+    that many threads."""
+    if args.workload != "decim":
+        return None
+    lib = _ref_decim_lib()
+    if lib is None:
+        return None
+    n = min(1 << 22, args.samples)
+    n -= n % 4
+    reps = 4
+    model = _cpu_model()
+
+    def fig(pins, what):
+        rate, wall = _ref_threads(lib, pins, n, reps)
+        return {"value": round(rate / 1e6, 3), "unit": "Msamples/s", "cores": len(pins), "kind": "reference",
+                "sample": f"{len(pins)} threads ({what}) x {reps} x {n} samples (channel i of the synthetic "
+                          f"workload on thread i, one FilterDnsamplingFir per thread), {wall:.2f} s wall; "
+                          f"oracle/_ref/strict/libref_decim_old.so; host CPU: {model}"}
+
+    if threads is not None:
+        return fig([None] * threads, "caller-set, unpinned")
+    cpus, phys = cpu_topology()
+    share, share_note = host_cores()
+    out = fig(cpus, f"every hardware thread of the affinity mask, machine nproc {os.cpu_count()}")
+    out["physical_cores"] = fig(phys, "one per physical core")
+    out["job_share"] = fig(cpus[:share], share_note)
+    return out
 
 
 def _cpu_model():
@@ -700,17 +838,103 @@ def pmc_traffic(args, work_name, per_launch_samples):
     return e.get("hbm_bytes_per_launch"), "rocprofv3 PMC, " + e.get("correction", "")
 
 
+# ---------------------------------------------------------------- parity
+def _load_digests(path):
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+def channel_parity(work, args, rank, table) -> dict:
+    """Cross-rank parity of the decim workload (outputs on 1/2/4/8
+    GPUs bit-identical to 1), checked after the timed region: every filter of
+    the rank is reset() (dnsampling_filters.h:56-60) and stepped once over its
+    resident channel(s), and the sha256 of each channel's output is compared
+    with tests/golden/channel_digests.json (made offline from the oracle and
+    the reference build by tests/golden/gen_channel_digests.py, for channel
+    ids rank * C + c).  Returns this rank's counts; reduce_parity() sums them
+    over ranks.  The outputs stay in work.y for the gather."""
+    import concurrent.futures as cf
+    import hashlib
+    C_ = work.C
+    first = rank * C_
+    want = ((table or {}).get("digests", {}).get(args.fp, {}).get(str(work.L), {}))
+    for f in work.f:
+        f.reset()
+    work.step()
+    DEV.synchronize()
+
+    def one(k):
+        return hashlib.sha256(work.y[k].cpu().numpy().tobytes()).hexdigest()
+
+    with cf.ThreadPoolExecutor(min(8, C_)) as ex:
+        got = list(ex.map(one, range(C_)))
+    checked = mism = missing = 0
+    bad = []
+    for k, h in enumerate(got):
+        w = want.get(str(first + k))
+        if w is None:
+            missing += 1
+        elif w == h:
+            checked += 1
+        else:
+            checked += 1
+            mism += 1
+            bad.append(first + k)
+    return {"channels_checked": checked, "mismatches": mism, "missing": missing, "bad_channels": bad}
+
+
+def gathered_parity(bufs, args, L, table) -> dict:
+    """Rank 0: the same digests over what the gather delivered (rank r's block
+    holds channels 8r..8r+7), so the collective's bytes are checked too."""
+    import concurrent.futures as cf
+    import hashlib
+    want = ((table or {}).get("digests", {}).get(args.fp, {}).get(str(L), {}))
+    jobs = [(r, k) for r in range(len(bufs)) for k in range(bufs[r].shape[0])]
+
+    def one(rk):
+        r, k = rk
+        return rk, hashlib.sha256(bufs[r][k].cpu().numpy().tobytes()).hexdigest()
+
+    checked = mism = missing = 0
+    per = bufs[0].shape[0]
+    with cf.ThreadPoolExecutor(8) as ex:
+        for (r, k), h in ex.map(one, jobs):
+            w = want.get(str(r * per + k))
+            if w is None:
+                missing += 1
+            else:
+                checked += 1
+                mism += int(w != h)
+    return {"channels_checked": checked, "mismatches": mism, "missing": missing}
+
+
+def reduce_parity(p: dict, world: int) -> dict:
+    """SUM of the per-rank counts over ranks (bad channel ids: rank 0's view
+    plus the total count)."""
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor([p["channels_checked"], p["mismatches"], p["missing"]], dtype=torch.int64,
+                         device=COLL_DEV)
+        dist.all_reduce(t)
+        p = dict(p, channels_checked=int(t[0]), mismatches=int(t[1]), missing=int(t[2]))
+    return p
+
+
 # ---------------------------------------------------------------- timing
 def timed_steps(work, args, world, torch):
     """W untimed warm-up steps, then K timed steps bracketed by barrier +
     synchronize on both sides.  Returns (max-over-ranks wall seconds, the HIP
     event duration of every timed step in ms, on the launch stream)."""
     from srcdsp_amd.dist import max_over_ranks
-    stream = torch.cuda.current_stream()
+    stream = DEV.stream()
     for _ in range(args.warmup):
         work.step()
     barrier(world)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    ev = [DEV.event_pair() for _ in range(args.steps)]
     barrier(world)
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -723,7 +947,7 @@ def timed_steps(work, args, world, torch):
     return wall, [a.elapsed_time(b) for a, b in ev]
 
 
-def measure_share(S, torch, args, world, rank, L, slay) -> dict:
+def measure_share(S, torch, args, world, rank, L, slay, table=None) -> dict:
     """configs[2]'s per-GPU share beside the main series: 8 channels of 2^28
     per GPU, one batched step per rank, same warm-up/steps protocol (it runs
     right after the main series, on a warm chip); then the RCCL gather of every
@@ -743,25 +967,34 @@ def measure_share(S, torch, args, world, rank, L, slay) -> dict:
                         "channels_per_launch": slay["channels_per_gpu"], "kernel_ms": round(kern_avg_ms, 4),
                         "algorithmic_bytes_per_launch": int(work.bytes_per_sample * per_launch)},
            "timed": "after the main series (warm chip); batched step over the rank's 8 channels"}
+    if not args.no_parity:
+        # after the timed steps: a fresh step per channel, digests vs the table
+        out["parity"] = reduce_parity(channel_parity(work, args, rank, table), world)
     if world > 1 and not args.no_gather:
         barrier(world)
         g0 = time.perf_counter()
         bufs = gather_to_root(work.y if COLL_DEV else work.y.cpu(), world, rank)
         barrier(world)
         gather_ms = (time.perf_counter() - g0) * 1e3
-        del bufs
         nbytes = int(world * work.y.numel() * work.y.element_size())
         assert nbytes == slay["gather_bytes"]
         out.update(gather_ms=round(gather_ms, 3), gather_bytes=nbytes,
                    gather_gbs=round(nbytes / (gather_ms * 1e-3) / 1e9, 1))
+        if rank == 0 and not args.no_parity:
+            out["gather_parity"] = gathered_parity(bufs, args, L, table)
+        del bufs
     del work
-    torch.cuda.empty_cache()
+    DEV.empty_cache()
     return out
 
 
 # ---------------------------------------------------------------- main
-def main():
-    args = parse()
+def main(argv=None, S=None, dev=None):
+    """argv: the command line (default sys.argv); S: the operator package
+    (default srcdsp_amd, the HIP library); dev: CudaDevice() by default.  The
+    CPU rehearsal passes a host stand-in for S and HostDevice()."""
+    global DEV
+    args = parse(argv)
     rc = spawn_ranks(args)
     if rc is not None:
         sys.exit(rc)
@@ -769,6 +1002,7 @@ def main():
         dry_run(args)
         return
     import torch
+    DEV = dev if dev is not None else CudaDevice()
     world, rank, local = dist_setup(args)
     reported = world
     if world > 1:
@@ -777,7 +1011,8 @@ def main():
     if world != args.gpus or reported != args.gpus:
         raise SystemExit(f"bench: --gpus {args.gpus} but the launcher started {world} rank(s) "
                          f"(process group: {reported})")
-    import srcdsp_amd as S
+    if S is None:
+        import srcdsp_amd as S
     S.lib()  # loud failure if the HIP library is missing
     if args.samples is None:
         args.samples = (1 << 26) if args.workload == "corr" else (1 << 28)
@@ -789,6 +1024,10 @@ def main():
     work_name, work_dtype = work.name, work.dtype
     wall, kern_ms = timed_steps(work, args, world, torch)
     kern_avg_ms = float(np.mean(kern_ms))
+    table = parity = None
+    if args.workload == "decim" and not args.no_parity:  # outside the timed region
+        table = _load_digests(args.digests)
+        parity = reduce_parity(channel_parity(work, args, rank, table), world)
     if args.dump_steps and rank == 0:
         print("step_ms " + " ".join(f"{v:.4f}" for v in kern_ms), file=sys.stderr, flush=True)
 
@@ -860,7 +1099,7 @@ def main():
 
     share = None
     if slay is not None:  # beside the main workload's buffers (2.5 GiB): HBM holds both
-        share = measure_share(S, torch, args, world, rank, L, slay)
+        share = measure_share(S, torch, args, world, rank, L, slay, table)
 
     if rank == 0:
         cfg = {"workload": work_name, "samples_per_channel": L, "channels_per_gpu": args.channels_per_gpu,
@@ -888,6 +1127,12 @@ def main():
             # `roofline` is rank 0's own launch(es): per GPU, the same work at every N
             roof["per_gpu"] = True
             roof["channels_per_launch"] = args.channels_per_gpu
+        if parity is not None:
+            line["parity"] = dict(parity, digest_table=os.path.relpath(args.digests, ROOT), fp_contract=args.fp,
+                                  checked=("after the timed region: every rank resets its filters, steps its "
+                                           "resident channel(s) once, and compares sha256 of each channel's output "
+                                           "with the oracle/reference digest of that channel id; counts summed "
+                                           "over ranks"))
         if share is not None:
             line["configs2_share"] = share
         if args.workload == "corr":

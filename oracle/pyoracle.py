@@ -124,6 +124,7 @@ class Oracle:
             "corr_reset": _sig(lib, "orc_corr_reset", None, VP),
             "corr_step": _sig(lib, "orc_corr_step", I, VP, VP, L, VP),
             "corr_prime": _sig(lib, "orc_corr_prime", None, VP, VP, L),
+            "corr_registers": _sig(lib, "orc_corr_registers", None, VP, VP, L, VP, VP),
             "corr_bits": _sig(lib, "orc_corr_bit_samples", None, VP, VP),
             "corr_status": _sig(lib, "orc_corr_status", None, VP, VP, VP, VP, VP, VP),
             "corr_destroy": _sig(lib, "orc_corr_destroy", None, VP),
@@ -296,6 +297,16 @@ class _Corr(_Handle):
         """State after streaming x with no detection (not a reference call)."""
         x = as_kind(x, "ci16")
         self.o.f["corr_prime"](self._h, _ptr(x), len(x))
+
+    def registers(self, x):
+        """Stream x with no detection (not a reference call) and return every
+        sample's (corrValue[0], energyValue[0]) as uint32 arrays
+        (correlators.h:244-250)."""
+        x = as_kind(x, "ci16")
+        c = np.zeros(len(x), np.uint32)
+        e = np.zeros(len(x), np.uint32)
+        self.o.f["corr_registers"](self._h, _ptr(x), len(x), _ptr(c), _ptr(e))
+        return c, e
 
     def bit_samples(self):
         b = np.zeros((self.N, 2), np.int16)

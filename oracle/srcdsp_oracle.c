@@ -549,8 +549,11 @@ void orc_corr_reset(orc_corr *c) {  /* :146-159 */
 }
 
 /* step (correlators.h:209-303) */
-/* detect = 0: stream the samples without the detection test (orc_corr_prime) */
-static int corr_run(orc_corr *c, const int16_t *in, long n, int *corr_index, int detect) {
+/* detect = 0: stream the samples without the detection test (orc_corr_prime);
+ * corr_out / energy_out (may be NULL): each sample's corrValue[0] and
+ * energyValue[0] as computed at :244-250 */
+static int corr_run(orc_corr *c, const int16_t *in, long n, int *corr_index, int detect, uint32_t *corr_out,
+                    uint32_t *energy_out) {
     const long H = (long)c->H, S = (long)c->S, N = (long)c->N;
     for (long idx = 0; idx < n; ++idx) {
         long top = (long)c->top;
@@ -583,6 +586,8 @@ static int corr_run(orc_corr *c, const int16_t *in, long n, int *corr_index, int
         c->corr[1] = c->corr[0];
         int32_t ar = tr >> 2, ai = ti >> 2;
         c->corr[0] = (uint32_t)wadd(wmul(ar, ar), wmul(ai, ai));   /* :250 */
+        if (corr_out) corr_out[idx] = c->corr[0];
+        if (energy_out) energy_out[idx] = c->energy[0];
         if (detect && c->corr[1] > c->corr[2] && c->corr[1] > c->corr[0]) {  /* :262 */
             double cm = sqrt((double)c->corr[1]);
             double em = sqrt((double)c->energy[1]);
@@ -606,7 +611,7 @@ static int corr_run(orc_corr *c, const int16_t *in, long n, int *corr_index, int
 }
 
 int orc_corr_step(orc_corr *c, const int16_t *in, long n, int *corr_index) {
-    return corr_run(c, in, n, corr_index, 1);
+    return corr_run(c, in, n, corr_index, 1, NULL, NULL);
 }
 
 /* Not a reference call: the state the correlator has after streaming `in`
@@ -614,7 +619,18 @@ int orc_corr_step(orc_corr *c, const int16_t *in, long n, int *corr_index) {
  * buffer split over ranks finds the same first detection). */
 void orc_corr_prime(orc_corr *c, const int16_t *in, long n) {
     int dummy = 0;
-    (void)corr_run(c, in, n, &dummy, 0);
+    (void)corr_run(c, in, n, &dummy, 0, NULL, NULL);
+}
+
+/* Not a reference call: stream `in` like orc_corr_prime (no detection test,
+ * so no `break`) and record every sample's registers as the reference computes
+ * them before its peak test (correlators.h:244-250): corr_out[i] =
+ * corrValue[0], energy_out[i] = energyValue[0].  Test infrastructure for the
+ * integer matrix-core probe (scripts/tune/corr_mfma.py), which computes the
+ * same two values for every sample of the config-5 buffer. */
+void orc_corr_registers(orc_corr *c, const int16_t *in, long n, uint32_t *corr_out, uint32_t *energy_out) {
+    int dummy = 0;
+    (void)corr_run(c, in, n, &dummy, 0, corr_out, energy_out);
 }
 
 void orc_corr_bit_samples(const orc_corr *c, int16_t *out) { memcpy(out, c->bits, 4 * (size_t)c->N); }

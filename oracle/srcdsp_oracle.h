@@ -79,6 +79,7 @@ void orc_corr_set_pattern(orc_corr *c, const int32_t *pattern_ci32, double thres
 void orc_corr_reset(orc_corr *c);
 int orc_corr_step(orc_corr *c, const int16_t *in_ci16, long n, int *corr_index);
 void orc_corr_prime(orc_corr *c, const int16_t *in_ci16, long n);
+void orc_corr_registers(orc_corr *c, const int16_t *in_ci16, long n, uint32_t *corr_out, uint32_t *energy_out);
 void orc_corr_bit_samples(const orc_corr *c, int16_t *out_ci16);
 void orc_corr_status(const orc_corr *c, uint32_t *energy3, uint32_t *corr3, uint32_t *coeffs_energy,
                      int *coeff_scaling, double *threshold_factor);

@@ -116,3 +116,72 @@ def test_gpus_n_dry_run_world_and_labels(n):
         assert sh["gather_bytes"] == 8 * n * (1 << 26) * 8
         assert sh["baseline_config"] == ("configs[2]" if n == 8 else
                                          f"configs[2] per-GPU layout ({8 * n} of 64 channels)")
+
+
+def _host_ranks(n, extra_env=None, args=()):
+    """Run tests/bench_host_rank.py as n gloo ranks (the driver's `bench.py
+    --gpus n` path with host stand-ins for the operators and the device) and
+    return rank 0's JSON line."""
+    import json
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n), OMP_NUM_THREADS="1",
+               **(extra_env or {}))
+    cmd = [sys.executable, os.path.join(ROOT, "tests", "bench_host_rank.py"), "--gpus", str(n),
+           "--samples", str(1 << 20), "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-pcie", *args]
+    procs = [subprocess.Popen(cmd, env=dict(env, RANK=str(r), LOCAL_RANK=str(r)), stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for r in range(n)]
+    outs = [p.communicate(timeout=300) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-3000:]
+    lines = [l for l in outs[0][0].splitlines() if l.startswith("{")]
+    assert len(lines) == 1 and not any(l.startswith("{") for o, _ in outs[1:] for l in o.splitlines())
+    return json.loads(lines[0])
+
+
+DIGESTS = os.path.join(ROOT, "tests", "golden", "channel_digests.json")
+
+
+@pytest.mark.skipif(not os.path.exists(DIGESTS), reason="tests/golden/channel_digests.json not generated")
+def test_bench_main_two_ranks_end_to_end_on_host():
+    """bench.main() past timed_steps at --gpus 2 (gloo,
+    host stand-ins): the line is assembled, the main series' parity covers
+    channels 0 and 1, configs[2]'s share covers channels 0..15 on the ranks
+    and again after the gather at rank 0, all with 0 mismatches against the
+    committed digests."""
+    line = _host_ranks(2)
+    assert line["n_gpus"] == 2 and line["world_size_reported"] == 2 and line["backend"] == "gloo"
+    assert line["value"] > 0 and line["ms_per_step"] > 0 and line["steps"] == 2
+    assert line["config"]["channels_total"] == 2 and line["config"]["samples_per_channel"] == 1 << 20
+    p = line["parity"]
+    assert (p["channels_checked"], p["mismatches"], p["missing"]) == (2, 0, 0), p
+    sh = line["configs2_share"]
+    assert sh["channels_total"] == 16 and sh["gather_bytes"] == 16 * (1 << 18) * 8
+    assert (sh["parity"]["channels_checked"], sh["parity"]["mismatches"]) == (16, 0), sh["parity"]
+    assert (sh["gather_parity"]["channels_checked"], sh["gather_parity"]["mismatches"]) == (16, 0)
+
+
+@pytest.mark.skipif(not os.path.exists(DIGESTS), reason="tests/golden/channel_digests.json not generated")
+def test_bench_parity_reports_a_corrupted_channel():
+    """One flipped input sample on channel 9 (rank 1's share, not rank 0's):
+    the summed counts over ranks and the gathered check both show exactly one
+    mismatching channel; the main series (channels 0, 1) stays clean."""
+    line = _host_ranks(2, {"STUB_CORRUPT_CHANNEL": "9"})
+    assert line["parity"]["mismatches"] == 0
+    assert line["configs2_share"]["parity"]["mismatches"] == 1
+    assert line["configs2_share"]["gather_parity"]["mismatches"] == 1
+
+
+@pytest.mark.skipif(not os.path.exists(DIGESTS), reason="tests/golden/channel_digests.json not generated")
+def test_bench_main_one_rank_with_share_on_host():
+    """The N = 1 path (no process group) with --share: one channel in the main
+    series, 8 in the share, no gather."""
+    line = _host_ranks(1, args=("--share",))
+    assert line["n_gpus"] == 1 and line["backend"] is None
+    assert line["parity"]["channels_checked"] == 1 and line["parity"]["mismatches"] == 0
+    sh = line["configs2_share"]
+    assert sh["parity"]["channels_checked"] == 8 and "gather_ms" not in sh

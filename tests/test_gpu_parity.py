@@ -581,9 +581,16 @@ def test_decim_errors_and_empty(S):
 
 def test_headline_whole_output(S, O):
     """Config 2 at full size (2^28 complex<float> samples, device-resident, one
-    step()): EVERY one of the 2^26 outputs against the oracle (FMA contract),
-    run in parallel windows on the host (tests/fullsize.py); the device
-    generator equals the host one on the first, a seam and the last window."""
+    step()), both float contracts: EVERY one of the 2^26 outputs
+    of the FMA contract against the FMA oracle, and of the strict contract
+    (SRCDSP_FLAG_FP_STRICT: a rounded multiply then a rounded add per tap, the
+    reference's own makefile build has no FMA, makefile:17;
+    dnsampling_filters.h:150-167) against the strict oracle, byte for byte;
+    then the stated tolerance over all 2^26 outputs: the FMA contract differs
+    from the strict reference by at most 1 output LSB (|delta| <= 1.0 on a
+    component) on at most 1e-4 of the outputs.  The oracle runs in parallel
+    windows on the host (tests/fullsize.py); the device generator equals the
+    host one on the first, a seam and the last window."""
     import torch
     import fullsize as F
     from srcdsp_amd.design import hamming_sinc
@@ -591,24 +598,32 @@ def test_headline_whole_output(S, O):
     L = 1 << 28
     x = torch.empty(L, dtype=torch.complex64, device="cuda")
     S.fill_synthetic(x, "cf32", seed=0x5EED, channel=0)
-    y = S.FilterDnsamplingFir(c, 4, fp="fma").step(x)
-    torch.cuda.synchronize()
+    y = {fp: S.FilterDnsamplingFir(c, 4, fp=fp).step(x).cpu().numpy() for fp in ("fma", "strict")}
     xh = x.cpu().numpy()
+    del x
+    torch.cuda.empty_cache()
     for lo in (0, (1 << 27) - 5000, L - 8192):
         assert np.array_equal(xh[lo:lo + 8192], O["fma"].gen_cf32(0x5EED, 0, lo, 8192)), lo
-    want = F.decim_all(lambda: O["fma"].decim(0, 4, c), xh, 4, 128, np.empty(L // 4, np.complex64))
-    bad = F.first_bad(y.cpu().numpy(), want)
-    assert bad is None, f"first differing output {bad}"
-    del x, y
-    torch.cuda.empty_cache()
+    want = {}
+    for fp in ("fma", "strict"):
+        want[fp] = F.decim_all(lambda: O[fp].decim(0, 4, c), xh, 4, 128, np.empty(L // 4, np.complex64))
+        bad = F.first_bad(y[fp], want[fp])
+        assert bad is None, f"fp={fp}: first differing output {bad}"
+    del xh
+    d = np.abs(y["fma"].view(np.float32) - want["strict"].view(np.float32)).reshape(-1, 2)
+    assert d.max() <= 1.0, f"max |fma - strict reference| = {d.max()}"
+    n_diff = int(np.count_nonzero(d.max(axis=1)))
+    assert n_diff <= 1e-4 * len(d), f"{n_diff} of {len(d)} outputs differ from the strict reference"
 
 
-def test_config3_per_gpu_share_whole_channel(S, O):
+def test_config3_per_gpu_share_whole_channels(S, O):
     """Config 3's per-GPU share at full size: 8 channels x 2^28 complex<float>
     samples (channels 8..15 of the 64, i.e. rank 1 of 8), one batched step as
-    bench.py --gpus N runs it.  One whole channel (all 2^26 outputs) against
-    the oracle; spot windows of the seven others (first tiles, a seam, random
-    interior, last tile); each channel's history is its own tail."""
+    bench.py --gpus N runs it.  EVERY output of all 8 channels (8 x 2^26)
+    against the oracle, channel by channel, so a grid.y / channel-stride
+    mapping error on any channel fails; each channel's input equals the host
+    generator on a first, an interior and a last window; each channel's
+    history is its own tail."""
     import torch
     import fullsize as F
     from srcdsp_amd.design import hamming_sinc
@@ -622,30 +637,16 @@ def test_config3_per_gpu_share_whole_channel(S, O):
     fs = [S.FilterDnsamplingFir(c, 4, fp="fma") for _ in range(C)]
     S.decim_step_batched(fs, x, y)
     torch.cuda.synchronize()
-    full = 5  # channel 13
-    xh = x[full].cpu().numpy()
-    want = F.decim_all(lambda: O["fma"].decim(0, 4, c), xh, 4, 128, np.empty(L // 4, np.complex64))
-    bad = F.first_bad(y[full].cpu().numpy(), want)
-    assert bad is None, f"channel {ch0 + full}: first differing output {bad}"
-    del xh, want
-    rng = np.random.default_rng(3)
-    n_out = L // 4
+    want = np.empty(L // 4, np.complex64)
     for k in range(C):
-        if k == full:
-            continue
-        starts = [0, 2048 - 3, n_out - 1000] + list(rng.integers(40, n_out - 1000, 3))
-        for s0 in starts:
-            s0 = int(s0)
-            lo = max(0, 4 * s0 - 128)
-            xin = x[k, lo:4 * (s0 + 64)].cpu().numpy()
-            assert np.array_equal(xin, O["fma"].gen_cf32(0x5EED, ch0 + k, lo, len(xin))), (k, s0)
-            r = O["fma"].decim(0, 4, c).step(xin)[(4 * s0 - lo) // 4:]
-            got = y[k, s0:s0 + 64].cpu().numpy()
-            assert np.array_equal(got, r[:len(got)]), (k, s0)
-    # the channels are independent objects: their histories are their own tails
-    for k in (0, C - 1):
-        h = fs[k].state()["history"]
-        assert h.tobytes() == x[k, L - 126:].cpu().numpy().tobytes(), k
+        xh = x[k].cpu().numpy()
+        for lo in (0, (1 << 27) + 12345, L - 8192):
+            assert np.array_equal(xh[lo:lo + 8192], O["fma"].gen_cf32(0x5EED, ch0 + k, lo, 8192)), (k, lo)
+        F.decim_all(lambda: O["fma"].decim(0, 4, c), xh, 4, 128, want)
+        bad = F.first_bad(y[k].cpu().numpy(), want)
+        assert bad is None, f"channel {ch0 + k}: first differing output {bad}"
+        assert fs[k].state()["history"].tobytes() == xh[L - 126:].tobytes(), k
+        del xh
     del x, y
     torch.cuda.empty_cache()
 
