@@ -80,6 +80,15 @@ public:
         : h_(o.h_), fenergy(std::move(o.fenergy)), fcorr(std::move(o.fcorr)), fthreshold(std::move(o.fthreshold)) {
         o.h_ = nullptr;
     }
+    // the reference's implicit move assignment (its ofstream members are
+    // move-assignable): take o's handle and streams, o keeps ours to destroy
+    FixedPatternCorrelator &operator=(FixedPatternCorrelator &&o) noexcept {
+        std::swap(h_, o.h_);
+        fenergy = std::move(o.fenergy);
+        fcorr = std::move(o.fcorr);
+        fthreshold = std::move(o.fthreshold);
+        return *this;
+    }
 #endif
 
     /// correlators.h:209-303

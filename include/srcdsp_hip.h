@@ -365,6 +365,11 @@ SRCDSP_API int srcdsp_decim_sharded_gather(srcdsp_decim_sharded_t h, void *const
 SRCDSP_API const char *srcdsp_last_error(void);
 /* Library version "major.minor.patch" and the offload target it was built for. */
 SRCDSP_API const char *srcdsp_version(void);
+/* Test switches this library was built with, read back from a kernel of this
+ * library: 0 for the shipped build; SRCDSP_BUILD_CORR_ALWAYS_EXACT for the
+ * test-only always-exact correlator build (tests/_build/). */
+#define SRCDSP_BUILD_CORR_ALWAYS_EXACT 1u
+SRCDSP_API int srcdsp_build_flags(unsigned *flags);
 /* Fill d_out with the counter-based synthetic samples the benchmarks use
  * (SURVEY.md §8d): component c of sample i (global index off+i) is
  * lo + (splitmix64((seed ^ channel<<40) + 2(off+i) + c) >> 32) mod (hi-lo+1).

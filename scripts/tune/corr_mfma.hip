@@ -1,0 +1,259 @@
+// Config 5's correlator on the integer matrix cores: a TUNING PROBE, not the
+// product (BASELINE north_star says the product path uses no
+// MFMA, so this kernel never ships in libsrcdsp_hip.so).
+//
+// What it computes, for every sample i of one fresh FixedPatternCorrelator<
+// int16_t, int32_t, 1024, 1> stream (history zeros before sample 0): the two
+// registers the reference forms before its peak test (correlators.h:233-250)
+//   C_i    = sum_k x[i - 1023 + k] * c[k]           complex, int32 wrap
+//            (c = conj(pattern), dsp_complex.cpp:31-37 products)
+//   corr_i = ((C_i.re >> cs) >> 2)^2 + ((C_i.im >> cs) >> 2)^2   uint32
+//   e_i    = (sum_k |x[i - 1023 + k]|^2) >> (cs / 2)             uint32 wrap
+// and stores both (8 B per sample) for a bit-exact comparison with the oracle.
+//
+// Formulation (exact modulo 2^32, as the reference's wrap-around sums):
+// * Limbs.  x = 256 xh + xl + 128 with xh = x >> 8 (the int16's high byte) and
+//   xl = (x & 255) - 128 (its low byte XOR 0x80), both in [-128, 127]; a zero
+//   sample (the history before the stream) is (0, -128).  A coefficient value
+//   v = 256 vh + vl, vl in [-128, 127], vh = (v - vl) / 256 (the host checks
+//   vh in [-128, 127]).  So x * v = 65536 xh vh + 256 (xh vl + xl vh) + xl vl
+//   + 128 v, and the window's sum of the last term is the constant
+//   bias = 128 sum_k v[k] (every window holds all 1024 taps).
+// * Toeplitz tiles.  A wave's tile is 1024 consecutive outputs
+//   i = i_w + 32 row + col (row, col in 0..31).  For chunk t (0..65) of 16
+//   samples, A_t[row][(s, comp)] = limb of x_comp[i_w + 32 row - 1024 + 16 t + s]
+//   (a pure reshape of the staged stream: row r of chunk t is the 16 samples at
+//   32 r + 16 t) and B_t[(s, comp)][col] = limb of the coefficient of output
+//   col for that sample, k = 16 t + s - col - 1 (zero outside [0, 1023]).
+//   66 chunks cover every (output, tap) pair exactly once: 1056 / 1024 = 3 %
+//   zero products.  Per chunk: 2 A fragments (xl, xh) and 4 B fragments
+//   (re/im output x low/high coefficient limb), 8 v_mfma_i32_32x32x32_i8 into
+//   6 accumulators S0 = xl.vl, S1 = xl.vh + xh.vl, S2 = xh.vh per component;
+//   C = S0 + (S1 << 8) + (S2 << 16) + bias.
+// * K order.  The 32 k of a lane group hold 16 samples x (re, im); lane
+//   (row or col = l & 31, group h = l >> 5) holds samples 8h..8h+7, 16 bytes,
+//   in the same byte order for A and B (scripts/tune/mfma_i8_probe.py checks
+//   that the instruction sums A byte j of lane (r, h) with B byte j of lane
+//   (c, h) for every j and h).
+// * LDS.  A: two byte planes (xl, xh), (re, im) per sample, 16 B pad per 32
+//   samples (row stride 80 B: the 16 lanes of a ds_read_b128 quarter hit 16
+//   different bank quads).  B: per kind, 4 copies of the limb array shifted by
+//   0..3 entries so every lane's 8 entries start 8-B aligned (2 ds_read_b64);
+//   built on the host, copied once per workgroup.  Energy: the inclusive
+//   prefix P of |x|^2 over the staged span (uint32 wrap), e_i = P[i] - P[i-1024].
+// * Grid.  Persistent, one 512-lane workgroup per CU (8 waves, 2 per SIMD),
+//   8192 outputs per workgroup tile.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v2i __attribute__((ext_vector_type(2)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+namespace {
+constexpr int NP = 1024;                 // pattern length (config 5)
+constexpr int WAVES = 8;
+constexpr int LANES = 64 * WAVES;
+constexpr int TILE = 1024 * WAVES;       // outputs per workgroup tile
+constexpr int SPAN = TILE + NP;          // staged samples per tile
+constexpr int GROUPS = SPAN / 32;        // 32-sample groups
+constexpr int PLANE = GROUPS * 80;       // bytes per limb plane (64 B data + 16 B pad per group)
+constexpr int CHUNKS = (NP + 32) / 16;   // 66
+constexpr int BENT = 1096;               // entries per B copy (2 B each)
+constexpr int BSTRIDE = 2240;            // bytes per B copy
+constexpr int BKIND = 4 * BSTRIDE;       // 4 shifted copies per kind
+constexpr int BBYTES = 4 * BKIND;        // 4 kinds: re lo, re hi, im lo, im hi
+constexpr int LDS_A = 2 * PLANE;
+constexpr int LDS_P = SPAN * 4;
+constexpr int LDS_TOTAL = BBYTES + LDS_A + LDS_P + WAVES * 4;
+static_assert(SPAN % 32 == 0 && TILE % 8192 == 0, "tile shape");
+static_assert(LDS_TOTAL <= 160 * 1024, "LDS");
+}  // namespace
+
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
+{
+    return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+__global__ void __launch_bounds__(LANES, 1)
+corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ btab, int cs, uint32_t bias_re,
+             uint32_t bias_im, uint32_t* __restrict__ corr_out, uint32_t* __restrict__ e_out, long n_tiles,
+             int store_all)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    unsigned char* ldsB = lds;
+    unsigned char* ldsA = lds + BBYTES;                 // xl plane, then xh plane
+    uint32_t* ldsP = (uint32_t*)(lds + BBYTES + LDS_A);  // prefix of |x|^2
+    uint32_t* ldsW = ldsP + SPAN;                        // per-wave totals of the scan
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int w = tid >> 6;
+    const int h = lane >> 5;
+    const int rc = lane & 31;  // A row / B col / D col
+
+    // B tables, once per workgroup
+    for (int i = tid; i < BBYTES / 16; i += LANES)
+        ((v4u*)ldsB)[i] = btab[i];
+
+    // per-lane LDS bases
+    // A: group 32 w + row (+ t >> 1), byte 32 (t & 1) + 16 h
+    const int a_base = 80 * (32 * w + rc) + 16 * h;
+    // B: copy sigma = (col + 1) & 3, entry e = 16 t + 8 h - col + 31 + sigma (multiple of 4)
+    const int sig = (rc + 1) & 3;
+    const int b_base = sig * BSTRIDE + 2 * (8 * h - rc + 31 + sig);
+
+    // next tile's input, fetched into registers before the current tile's
+    // MFMA work: granule g = tid + 512 k of the span; the buffer descriptor's
+    // range check returns zeros past the end and, through the wrapped 32-bit
+    // offset, before sample 0 (tile 0's history), i.e. the limbs of 0
+    constexpr int NG = (SPAN / 4 + LANES - 1) / LANES;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)(4 * n), 0x00020000);
+    v4u pre[NG];
+    auto fetch = [&](long tile) {
+        const long j0 = tile * TILE - NP;
+#pragma unroll
+        for (int k = 0; k < NG; ++k) {
+            const int g = tid + LANES * k;
+            const uint32_t voff = (uint32_t)(4 * (j0 + 4 * g));
+            pre[k] = v4u{0u, 0u, 0u, 0u};
+            if (g < SPAN / 4)
+                pre[k] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 0));
+        }
+    };
+    if (blockIdx.x < n_tiles) fetch(blockIdx.x);
+
+    for (long tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+        const long i0 = tile * TILE;
+        __syncthreads();          // previous tile's readers are done with A and P
+        // ---- staging: the prefetched granules -> limb planes and |x|^2
+#pragma unroll
+        for (int k = 0; k < NG; ++k) {
+            const int g = tid + LANES * k;
+            if (g >= SPAN / 4) break;
+            const v4u v = pre[k];
+            const int js = 4 * g;
+            const int off = 80 * (js >> 5) + 2 * (js & 31);
+            uint32_t lo0 = perm(v[1], v[0], 0x06040200u) ^ 0x80808080u;
+            uint32_t lo1 = perm(v[3], v[2], 0x06040200u) ^ 0x80808080u;
+            uint32_t hi0 = perm(v[1], v[0], 0x07050301u);
+            uint32_t hi1 = perm(v[3], v[2], 0x07050301u);
+            *(v2i*)(ldsA + off) = v2i{(int)lo0, (int)lo1};
+            *(v2i*)(ldsA + PLANE + off) = v2i{(int)hi0, (int)hi1};
+            v4u p;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {  // |x|^2 = re^2 + im^2, int32 wrap (correlators.h:237)
+                const int re = (int16_t)(v[q] & 0xFFFFu), im = (int16_t)(v[q] >> 16);
+                p[q] = (uint32_t)re * (uint32_t)re + (uint32_t)im * (uint32_t)im;
+            }
+            *(v4u*)(ldsP + js) = p;
+        }
+        __syncthreads();
+        if (tile + gridDim.x < n_tiles) fetch(tile + gridDim.x);
+        // ---- energy: inclusive prefix of |x|^2 over the span (18 samples per lane)
+        {
+            constexpr int PER = SPAN / LANES;  // 18
+            static_assert(SPAN % LANES == 0, "scan split");
+            uint32_t loc[PER];
+            uint32_t s = 0;
+#pragma unroll
+            for (int q = 0; q < PER; ++q) {
+                s += ldsP[PER * tid + q];
+                loc[q] = s;
+            }
+            // wave-inclusive scan of the lane totals
+            uint32_t incl = s;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                uint32_t o = __shfl_up(incl, d, 64);
+                if (lane >= d) incl += o;
+            }
+            if (lane == 63) ldsW[w] = incl;
+            __syncthreads();
+            uint32_t base = incl - s;
+            for (int q = 0; q < w; ++q) base += ldsW[q];
+#pragma unroll
+            for (int q = 0; q < PER; ++q)
+                ldsP[PER * tid + q] = loc[q] + base;
+        }
+        __syncthreads();
+
+        // ---- correlation: 66 chunks x 8 MFMAs into 6 accumulators
+        v16i s0r = {}, s1r = {}, s2r = {}, s0i = {}, s1i = {}, s2i = {};
+        const unsigned char* pa = ldsA + a_base;
+        const unsigned char* pb = ldsB + b_base;
+#pragma unroll 2
+        for (int t = 0; t < CHUNKS; ++t) {
+            const int ao = 80 * (t >> 1) + 32 * (t & 1);
+            const v4i axl = *(const v4i*)(pa + ao);
+            const v4i axh = *(const v4i*)(pa + PLANE + ao);
+            const int bo = 32 * t;
+            v2i b0a = *(const v2i*)(pb + bo), b0b = *(const v2i*)(pb + bo + 8);
+            v2i b1a = *(const v2i*)(pb + BKIND + bo), b1b = *(const v2i*)(pb + BKIND + bo + 8);
+            v2i b2a = *(const v2i*)(pb + 2 * BKIND + bo), b2b = *(const v2i*)(pb + 2 * BKIND + bo + 8);
+            v2i b3a = *(const v2i*)(pb + 3 * BKIND + bo), b3b = *(const v2i*)(pb + 3 * BKIND + bo + 8);
+            const v4i brl = {b0a[0], b0a[1], b0b[0], b0b[1]};
+            const v4i brh = {b1a[0], b1a[1], b1b[0], b1b[1]};
+            const v4i bil = {b2a[0], b2a[1], b2b[0], b2b[1]};
+            const v4i bih = {b3a[0], b3a[1], b3b[0], b3b[1]};
+            s0r = __builtin_amdgcn_mfma_i32_32x32x32_i8(axl, brl, s0r, 0, 0, 0);
+            s0i = __builtin_amdgcn_mfma_i32_32x32x32_i8(axl, bil, s0i, 0, 0, 0);
+            s1r = __builtin_amdgcn_mfma_i32_32x32x32_i8(axl, brh, s1r, 0, 0, 0);
+            s1i = __builtin_amdgcn_mfma_i32_32x32x32_i8(axl, bih, s1i, 0, 0, 0);
+            s1r = __builtin_amdgcn_mfma_i32_32x32x32_i8(axh, brl, s1r, 0, 0, 0);
+            s1i = __builtin_amdgcn_mfma_i32_32x32x32_i8(axh, bil, s1i, 0, 0, 0);
+            s2r = __builtin_amdgcn_mfma_i32_32x32x32_i8(axh, brh, s2r, 0, 0, 0);
+            s2i = __builtin_amdgcn_mfma_i32_32x32x32_i8(axh, bih, s2i, 0, 0, 0);
+        }
+
+        // ---- epilogue: D layout col = l & 31, row = (r & 3) + 8 (r >> 2) + 4 h
+        const unsigned es = (unsigned)(cs / 2) & 31u;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+            const long i = i0 + 1024 * w + 32 * row + rc;
+            const uint32_t cr = (uint32_t)s0r[r] + ((uint32_t)s1r[r] << 8) + ((uint32_t)s2r[r] << 16) + bias_re;
+            const uint32_t ci = (uint32_t)s0i[r] + ((uint32_t)s1i[r] << 8) + ((uint32_t)s2i[r] << 16) + bias_im;
+            const int32_t tr = ((int32_t)cr >> (cs & 31)) >> 2;  // scale32 (dsp_complex.cpp:43-46), then :250
+            const int32_t ti = ((int32_t)ci >> (cs & 31)) >> 2;
+            const uint32_t corr = (uint32_t)tr * (uint32_t)tr + (uint32_t)ti * (uint32_t)ti;
+            // local sample index of output i: i - j0; window (i - 1024, i]
+            const int li = 1024 * w + 32 * row + rc + NP;
+            const uint32_t e = (ldsP[li] - ldsP[li - NP]) >> es;
+            if (i < n && (store_all || (corr == 0xFFFFFFFFu && e == 0xFFFFFFFFu))) {
+                corr_out[i] = corr;
+                e_out[i] = e;
+            }
+        }
+    }
+}
+
+extern "C" int tune_corr_mfma_lds_bytes() { return LDS_TOTAL; }
+extern "C" int tune_corr_mfma_btab_bytes() { return BBYTES; }
+extern "C" int tune_corr_mfma_geometry(int* out)
+{
+    out[0] = TILE; out[1] = CHUNKS; out[2] = BENT; out[3] = BSTRIDE; out[4] = BKIND; out[5] = BBYTES;
+    out[6] = PLANE; out[7] = LDS_TOTAL;
+    return 0;
+}
+
+extern "C" int tune_corr_mfma(const void* x, long n, const void* btab, int cs, uint32_t bias_re, uint32_t bias_im,
+                              void* corr_out, void* e_out, int grid, int store_all, hipStream_t s)
+{
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)corr_mfma_i8, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           LDS_TOTAL);
+        if (e != hipSuccess) return (int)e;
+        attr = true;
+    }
+    const long n_tiles = (n + TILE - 1) / TILE;
+    if (n % 4 != 0 || 4 * n >= (1l << 31)) return 1;  // granule loads and the wrapped-offset zero fill
+    if (grid <= 0) grid = 256;
+    if (grid > n_tiles) grid = (int)n_tiles;
+    hipLaunchKernelGGL(corr_mfma_i8, dim3(grid), dim3(LANES), LDS_TOTAL, s, (const uint32_t*)x, n,
+                       (const v4u*)btab, cs, bias_re, bias_im, (uint32_t*)corr_out, (uint32_t*)e_out, n_tiles,
+                       store_all);
+    return (int)hipGetLastError();
+}

@@ -1,0 +1,266 @@
+#!/usr/bin/env python3
+"""Config 5's correlator on the integer matrix cores (tuning probe, VERDICT r5
+item 3; the kernel is scripts/tune/corr_mfma.hip and never ships).
+
+1. Builds the config-5 buffer exactly as bench.py's corr workload (2^26
+   complex<int16_t>, noise +-125 and the +-1000 pattern copy at 3/4) and the
+   B tables of the limb formulation (corr_mfma.hip's header).
+2. Runs the probe with every sample's (corr, energy) registers stored and
+   compares ALL of them with the oracle (orc_corr_registers: the reference's
+   corrValue[0] / energyValue[0] of correlators.h:244-250 for every sample,
+   in parallel windows primed with their 1024-sample history), bit for bit.
+3. Times the probe (stores suppressed) and the product's corr_scan_s1 on the
+   same box with HIP events, and reports both per scanned sample against
+   their peaks: the I8 MFMA rate (32x32x32 i8: 32 cycles per SIMD = 1024 MACs
+   per clock per SIMD, 2.52e15 MAC/s at 2.4 GHz) and the v_dot2 rate the
+   product is graded on (39.3e12 lane-ops/s).
+
+--emulate N: no GPU; replays the kernel's lane fragments and table addresses
+in numpy for the first N outputs (N a multiple of 1024) and checks them
+against the oracle (validates the host tables and index algebra)."""
+import argparse
+import concurrent.futures as cf
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import pyoracle  # noqa: E402
+from srcdsp_amd.design import qpsk_pattern  # noqa: E402
+
+NP = 1024
+CHUNKS = 66
+BENT, BSTRIDE = 1096, 2240
+BKIND = 4 * BSTRIDE
+I8_PEAK = 1024 * 1024 * 2.4e9    # MACs/s: 1024 SIMDs x 1024 i8 MACs per clock (32x32x32 in 32 cycles)
+DOT2_PEAK = 39.32e12             # v_dot2 lane-ops/s (bench.py VALU_PEAK_TOPS)
+
+
+def config5_buffer(L):
+    """bench.py CorrWorkload's buffer (same RNG calls)."""
+    p = qpsk_pattern(1024, 500, seed=2)
+    rng = np.random.default_rng(0)
+    x = rng.integers(-125, 126, size=(L, 2)).astype(np.int32)
+    off = (3 * L) // 4
+    x[off:off + 1024] += 2 * p
+    return p, np.clip(x, -32768, 32767).astype(np.int16)
+
+
+def limbs(v):
+    """v (int64 array) = 256 vh + vl, vl in [-128, 127]."""
+    vl = ((v + 128) & 255) - 128
+    vh = (v - vl) >> 8
+    if vh.min() < -128 or vh.max() > 127:
+        raise ValueError("coefficient outside the 2-limb range (|v| >= 32640)")
+    return vl.astype(np.int8), vh.astype(np.int8)
+
+
+def btables(p):
+    """The kernel's LDS B image: 4 kinds (re lo, re hi, im lo, im hi) x 4
+    copies shifted by sigma; copy sigma entry e holds the coefficient pair of
+    tap k = e - sigma - 32 (zero outside [0, 1023]); pair = (comp 0, comp 1) =
+    re output: (c.re, -c.im) = (p.re, p.im); im output: (c.im, c.re) =
+    (-p.im, p.re), with c = conj(p) (correlators.h:173-176)."""
+    p = p.astype(np.int64)
+    pairs = {"re": np.stack([p[:, 0], p[:, 1]], 1), "im": np.stack([-p[:, 1], p[:, 0]], 1)}
+    img = np.zeros(4 * BKIND, np.uint8)
+    bias = {}
+    for ki, (out, limb) in enumerate([("re", 0), ("re", 1), ("im", 0), ("im", 1)]):
+        lo, hi = limbs(pairs[out])
+        v = (lo if limb == 0 else hi).view(np.uint8)  # (1024, 2)
+        bias[out] = int((128 * pairs[out].sum()) % (1 << 32))
+        for sig in range(4):
+            base = ki * BKIND + sig * BSTRIDE
+            e = np.arange(BENT)
+            k = e - sig - 32
+            ok = (k >= 0) & (k < NP)
+            a = np.zeros((BENT, 2), np.uint8)
+            a[ok] = v[k[ok]]
+            img[base:base + 2 * BENT] = a.reshape(-1)
+    return img, bias
+
+
+def coeff_scaling(p):
+    o = pyoracle.Oracle(0)
+    c = o.corr(NP, 1)
+    c.set_pattern(p)
+    return c.status()["coeff_scaling"]
+
+
+def oracle_registers(p, x, win=1 << 20, workers=16):
+    n = len(x)
+    corr = np.empty(n, np.uint32)
+    en = np.empty(n, np.uint32)
+
+    def job(s):
+        o = pyoracle.Oracle(0)
+        c = o.corr(NP, 1)
+        c.set_pattern(p)
+        if s:
+            c.prime(x[max(0, s - NP - 2):s])
+        a, b = c.registers(x[s:s + win])
+        corr[s:s + len(a)] = a
+        en[s:s + len(b)] = b
+
+    with cf.ThreadPoolExecutor(max(1, min(workers, os.cpu_count() or 1))) as ex:
+        list(ex.map(job, range(0, n, win)))
+    return corr, en
+
+
+def emulate(p, x, n_out):
+    """numpy replay of corr_mfma_i8's fragments for outputs [0, n_out)."""
+    img, bias = btables(p)
+    cs = coeff_scaling(p)
+    L = len(x)
+    xs = np.zeros((n_out + NP, 2), np.int64)  # staged samples j = -1024 .. n_out - 1
+    xs[NP:] = x[:n_out]
+    xl = (xs & 255) - 128  # the low byte XOR 0x80, as a signed byte
+    xh = (xs >> 8).astype(np.int64)
+    assert np.array_equal(256 * xh + xl + 128, xs)
+    kinds = img.view(np.int8).astype(np.int64)
+    corr = np.empty(n_out, np.uint32)
+    for iw in range(0, n_out, 1024):
+        acc = {k: np.zeros((32, 32), np.int64) for k in ("s0r", "s1r", "s2r", "s0i", "s1i", "s2i")}
+        for t in range(CHUNKS):
+            A = {}
+            for nm, pl in (("xl", xl), ("xh", xh)):
+                a = np.zeros((32, 2, 16), np.int64)  # [row][h][byte]
+                for h in range(2):
+                    j = iw + 32 * np.arange(32)[:, None] + 16 * t + 8 * h + np.arange(8)[None, :]  # local (+1024)
+                    a[:, h, :] = pl[j].reshape(32, 16)
+                A[nm] = a
+            B = {}
+            for ki, nm in enumerate(("rl", "rh", "il", "ih")):
+                b = np.zeros((32, 2, 16), np.int64)  # [col][h][byte]
+                for col in range(32):
+                    sig = (col + 1) & 3
+                    for h in range(2):
+                        addr = ki * BKIND + sig * BSTRIDE + 2 * (8 * h - col + 31 + sig) + 32 * t
+                        assert addr % 8 == 0
+                        b[col, h] = kinds[addr:addr + 16]
+                B[nm] = b
+
+            def mm(a, b):
+                return np.einsum("rhj,chj->rc", a, b)
+            acc["s0r"] += mm(A["xl"], B["rl"]); acc["s0i"] += mm(A["xl"], B["il"])
+            acc["s1r"] += mm(A["xl"], B["rh"]) + mm(A["xh"], B["rl"]); acc["s1i"] += mm(A["xl"], B["ih"]) + mm(A["xh"], B["il"])
+            acc["s2r"] += mm(A["xh"], B["rh"]); acc["s2i"] += mm(A["xh"], B["ih"])
+        m32 = (1 << 32) - 1
+        cr = (acc["s0r"] + (acc["s1r"] << 8) + (acc["s2r"] << 16) + bias["re"]) & m32
+        ci = (acc["s0i"] + (acc["s1i"] << 8) + (acc["s2i"] << 16) + bias["im"]) & m32
+        tr = (cr.astype(np.uint32).view(np.int32).astype(np.int64) >> cs) >> 2
+        ti = (ci.astype(np.uint32).view(np.int32).astype(np.int64) >> cs) >> 2
+        c = (tr * tr + ti * ti) & m32
+        corr[iw:iw + 1024] = c.reshape(-1).astype(np.uint32)  # row-major = i_w + 32 row + col
+    return corr
+
+
+def run_gpu(args, p, x):
+    import torch
+    lib = C.CDLL(os.path.join(HERE, "libcorrmfma.so"))
+    lib.tune_corr_mfma.argtypes = [C.c_void_p, C.c_long, C.c_void_p, C.c_int, C.c_uint32, C.c_uint32, C.c_void_p,
+                                   C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+    img, bias = btables(p)
+    cs = coeff_scaling(p)
+    n = len(x)
+    dx = torch.from_numpy(x).cuda()
+    db = torch.from_numpy(img).cuda()
+    dc = torch.zeros(n, dtype=torch.int32, device="cuda")
+    de = torch.zeros(n, dtype=torch.int32, device="cuda")
+    st = torch.cuda.current_stream()
+
+    def launch(store_all, grid=args.grid):
+        rc = lib.tune_corr_mfma(C.c_void_p(dx.data_ptr()), n, C.c_void_p(db.data_ptr()), cs, bias["re"], bias["im"],
+                                C.c_void_p(dc.data_ptr()), C.c_void_p(de.data_ptr()), grid, store_all,
+                                C.c_void_p(st.cuda_stream))
+        assert rc == 0, rc
+
+    out = {"samples": n, "coeff_scaling": cs, "bias": bias}
+    launch(1)
+    torch.cuda.synchronize()
+    got_c = dc.cpu().numpy().view(np.uint32)
+    got_e = de.cpu().numpy().view(np.uint32)
+    if not args.no_check:
+        t0 = time.time()
+        want_c, want_e = oracle_registers(p, x)
+        out["oracle_s"] = round(time.time() - t0, 1)
+        bc = np.nonzero(got_c != want_c)[0]
+        be = np.nonzero(got_e != want_e)[0]
+        out["corr_mismatches"] = int(len(bc))
+        out["energy_mismatches"] = int(len(be))
+        out["first_bad"] = [int(bc[0]) if len(bc) else None, int(be[0]) if len(be) else None]
+        print(json.dumps({"check": out}), flush=True)
+
+    def timeit(fn, reps):
+        for _ in range(args.warmup):
+            fn()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for a, b in ev:
+            a.record(st)
+            fn()
+            b.record(st)
+        torch.cuda.synchronize()
+        return [a.elapsed_time(b) for a, b in ev]
+
+    ms = timeit(lambda: launch(0), args.reps)
+    ms_store = timeit(lambda: launch(1), args.reps)
+    t = float(np.mean(ms)) * 1e-3
+    macs = 16896.0 * n  # 66 chunks x 8 MFMAs x 32768 MACs per 1024 outputs
+    out["probe"] = {"ms": round(float(np.mean(ms)), 4), "ms_min": round(float(np.min(ms)), 4),
+                    "ms_with_stores": round(float(np.mean(ms_store)), 4),
+                    "gsamples_per_s": round(n / t / 1e9, 2),
+                    "i8_macs_per_s": macs / t, "i8_peak_frac": round(macs / t / I8_PEAK, 4),
+                    "useful_frac_of_macs": round(16384 / 16896, 4),
+                    "note": "every sample's corr and energy registers; stores suppressed in 'ms'"}
+    # the product on the same box: corr_scan_s1 through the Python mirror (stops at the detection)
+    import srcdsp_amd as S
+    g = S.FixedPatternCorrelator(NP, 1)
+    g.setPattern(p)
+    res = {}
+
+    def prod():
+        g.reset()
+        res["r"] = g.step(dx)
+    pms = timeit(prod, args.reps)
+    found, idx = res["r"]
+    scanned = idx + 2 if found else n
+    tp = float(np.mean(pms)) * 1e-3
+    out["product"] = {"ms": round(float(np.mean(pms)), 4), "detection": [bool(found), int(idx)],
+                      "scanned_samples": int(scanned), "gsamples_per_s": round(scanned / tp / 1e9, 2),
+                      "dot2_peak_frac": round(2048.0 * scanned / tp / DOT2_PEAK, 4)}
+    out["speedup_per_sample"] = round((n / t) / (scanned / tp), 2)
+    out["bounds_gsamples_per_s"] = {"i8_mfma_limb_formulation": round(I8_PEAK / 16896 / 1e9, 1),
+                                    "v_dot2": round(DOT2_PEAK / 2048 / 1e9, 1)}
+    print(json.dumps(out), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--samples", type=int, default=1 << 26)
+    ap.add_argument("--emulate", type=int, default=0)
+    ap.add_argument("--grid", type=int, default=256)
+    ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--no-check", action="store_true")
+    args = ap.parse_args()
+    p, x = config5_buffer(args.samples)
+    if args.emulate:
+        n = args.emulate
+        got = emulate(p, x, n)
+        want, _ = oracle_registers(p, x[:n])
+        bad = np.nonzero(got != want)[0]
+        print(f"emulate: {n} outputs, {len(bad)} differ from the oracle" + (f" (first {bad[0]})" if len(bad) else ""))
+        sys.exit(1 if len(bad) else 0)
+    run_gpu(args, p, x)
+
+
+if __name__ == "__main__":
+    main()

@@ -105,6 +105,7 @@ SIGNATURES = {
     "srcdsp_decim_sharded_gather": (I, [VP, HP, SZ, SZ, VP, I]),
     "srcdsp_last_error": (C.c_char_p, []),
     "srcdsp_version": (C.c_char_p, []),
+    "srcdsp_build_flags": (C.c_int, [C.POINTER(C.c_uint)]),
     "srcdsp_fill_synthetic": (I, [VP, I, SZ, U64, U64, U64, I, I, VP]),
 }
 

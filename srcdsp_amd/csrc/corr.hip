@@ -766,7 +766,38 @@ static int corr_run(srcdsp_corr_state &c, const uint32_t *d_in, size_t n_, int *
 using namespace srcdsp;
 struct srcdsp_corr { srcdsp_corr_state c; };
 
+// The build's test switches, reported by a kernel of this library (so a
+// process holding two copies of the library -- the product and a test build,
+// tests/test_gpu_corr_hit.py -- can tell which copy's kernels a call ran).
+__global__ void corr_build_flags_kernel(unsigned *out) {
+    if (threadIdx.x == 0) {
+#ifdef SRCDSP_CORR_ALWAYS_EXACT
+        *out = SRCDSP_BUILD_CORR_ALWAYS_EXACT;
+#else
+        *out = 0u;
+#endif
+    }
+}
+
 extern "C" {
+
+SRCDSP_API int srcdsp_build_flags(unsigned *flags) {
+    SRCDSP_ARG_CHECK(flags != nullptr, "build_flags: null flags");
+    unsigned *d = nullptr;
+    if (hipMalloc(&d, sizeof(unsigned)) != hipSuccess) {
+        set_error("build_flags: device allocation failed");
+        return SRCDSP_ERR_HIP;
+    }
+    hipLaunchKernelGGL(corr_build_flags_kernel, dim3(1), dim3(64), 0, nullptr, d);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpy(flags, d, sizeof(unsigned), hipMemcpyDeviceToHost);
+    hipFree(d);
+    if (e != hipSuccess) {
+        set_error(hipGetErrorString(e));
+        return SRCDSP_ERR_HIP;
+    }
+    return SRCDSP_OK;
+}
 
 SRCDSP_API int srcdsp_corr_create(srcdsp_corr_t *out, unsigned N, unsigned S) {
     SRCDSP_ARG_CHECK(out != nullptr, "corr_create: null out");

@@ -374,6 +374,20 @@ def test_dropin_corr_debug_files_compile(tmp_path):
                             "-I", INC, "-I", "/opt/rocm/include", "-D__HIP_PLATFORM_AMD__", "-fsyntax-only",
                             os.path.join(ROOT, "tests", "cpp", "corr_debug_main.cpp")], capture_output=True, text=True)
         assert r.returncode == 0, r.stderr
+    # the move-only object under the macro: move construction AND move
+    # assignment (the reference's implicit ones), copies rejected
+    src = tmp_path / "corr_move.cpp"
+    src.write_text('#include <cmath>\n#include <cassert>\n#include <complex>\n#include <cstdint>\n#include <vector>\n#include <array>\n#include "correlators.h"\n#include <utility>\n'
+                   'int main() {\n  dsptl::FixedPatternCorrelator<int16_t, int32_t, 32, 4> a, b;\n'
+                   '  dsptl::FixedPatternCorrelator<int16_t, int32_t, 32, 4> c(std::move(a));\n'
+                   '  b = std::move(c);\n  return 0;\n}\n')
+    cmd = ["g++", "-std=gnu++11", "-Wall", "-DCREATE_DEBUG_FILES", "-I", INC, "-I", "/opt/rocm/include",
+           "-D__HIP_PLATFORM_AMD__", "-fsyntax-only", str(src)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    src.write_text(src.read_text().replace("b = std::move(c);", "b = c;"))
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode != 0 and "deleted" in r.stderr
 
 
 @pytest.mark.gpu

@@ -204,7 +204,20 @@ def _bind(lib):
 
 @pytest.fixture(scope="module")
 def exact_lib(S):
-    return _bind(C.CDLL(_need(EXACT), mode=C.RTLD_LOCAL))
+    lib = _bind(C.CDLL(_need(EXACT), mode=C.RTLD_LOCAL))
+    lib.srcdsp_build_flags.restype, lib.srcdsp_build_flags.argtypes = C.c_int, [C.POINTER(C.c_uint)]
+    return lib
+
+
+def test_exact_build_runs_its_own_kernels(S, exact_lib):
+    """the always-exact build is loaded RTLD_LOCAL beside the
+    product library (RTLD_GLOBAL) with the same exported names; a kernel of
+    each library reports its own build switch, so the sweep below really runs
+    the always-exact kernels and not the product's."""
+    f = C.c_uint(99)
+    assert exact_lib.srcdsp_build_flags(C.byref(f)) == 0 and f.value == 1  # SRCDSP_BUILD_CORR_ALWAYS_EXACT
+    f.value = 99
+    assert S.lib().srcdsp_build_flags(C.byref(f)) == 0 and f.value == 0
 
 
 @pytest.mark.parametrize("host", [False, True], ids=["device", "host"])
