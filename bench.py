@@ -40,6 +40,13 @@ sys.path.insert(0, ROOT)
 METRIC = "Msamples/sec (in) for 127-tap cplx<float> decim-4 polyphase FIR, 256 Msamp; %HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 VALU_PEAK_TOPS = 39.32  # 256 CUs x 4 SIMD x 16 lanes x 2.4 GHz, one v_dot2 each per clock
+# i8 matrix cores: v_mfma_i32_32x32x32_i8 in 32 cycles per SIMD = 1024 MACs per
+# clock per SIMD (MI355X_MICROARCH.md, I8 row: 2x BF16 per clock), x 1024 SIMDs x 2.4 GHz
+I8_MFMA_PEAK_MACS = 1024 * 1024 * 2.4e9
+# config 5 exactly on them (scripts/tune/corr_mfma.hip): 4 limb products x 4 real
+# products per complex tap = 16 i8 MACs, 1024 taps + the 3 % Toeplitz pad (66
+# sixteen-sample chunks per 1024 outputs) = 16896 MACs per output
+CORR_I8_MACS_PER_SAMPLE = 16896.0
 SEED = 0x5EED
 
 
@@ -1096,6 +1103,17 @@ def main(argv=None, S=None, dev=None):
                 "traffic": traffic, "traffic_source": traffic_note,
                 "kernel": work.name, "kernel_ms": round(kern_avg_ms, 4), "scanned_samples": int(scanned),
                 "hbm_gbs_for_reference": round(achieved, 1)}
+        # the chip-level bound of the same exact integer arithmetic (VERDICT r5
+        # item 3): on the i8 matrix cores through int8 limbs.  Measured by the
+        # tuning probe (bit-exact on every sample of this buffer),
+        # not shipped: north_star keeps this path on vector MACs.
+        rate = scanned / world / (kern_avg_ms * 1e-3)
+        i8 = I8_MFMA_PEAK_MACS / CORR_I8_MACS_PER_SAMPLE
+        roof["other_bound"] = {"bound": "mfma_i8", "achieved": round(rate / 1e9, 2), "peak": round(i8 / 1e9, 1),
+                               "unit": "Gsamples/s", "frac": round(rate / i8, 4),
+                               "formulation": "int8 limbs of the int16 samples and of the pattern, Toeplitz "
+                                              "32x32x32 tiles, 16896 i8 MACs per output (exact mod 2^32)",
+                               "probe": "scripts/tune/corr_mfma.py; profiles/tuning/r06_corr_mfma.json"}
 
     share = None
     if slay is not None:  # beside the main workload's buffers (2.5 GiB): HBM holds both

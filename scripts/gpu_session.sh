@@ -26,6 +26,10 @@
 #                    (scripts/tune/ab_libs.sh; WORKLOADS, ROUNDS, LAUNCHES)
 #   dist             the 2-rank GPU test of the N > 1 path (tests/test_gpu_dist.py)
 #   cpp              the drop-in C++ tests (tests/test_dropin_cpp.py -m gpu)
+#   mfma             the integer matrix-core probes (tuning only, never shipped): config 5's correlator
+#                    (scripts/tune/corr_mfma.py ${CORR_ARGS}) and config 4's tap loop
+#                    (scripts/tune/mixdecim_mfma.py ${MIX_ARGS}), each checked against the oracle and timed
+#                    beside the product on the same box
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -90,6 +94,14 @@ for s in ${STEPS:-smoke tests bench}; do
     census) step census_$TAG 120 python -u scripts/tune/census.py ;;
     ab) step ab_$TAG 1000 bash scripts/tune/ab_libs.sh ;;
     dist) step dist_$TAG 300 python -u -m pytest tests/test_gpu_dist.py -m gpu -v --timeout 240 --timeout-method thread ;;
+    mfma)
+      step corrmfma_$TAG 400 python -u scripts/tune/corr_mfma.py ${CORR_ARGS}
+      step mixmfma_$TAG 400 python -u scripts/tune/mixdecim_mfma.py ${MIX_ARGS} ;;
+    mfmapmc)  # SQ / MFMA counter passes of the two probes' kernels
+      step corrmfmapmc_$TAG 600 python -u scripts/tune/pmc_cmd.py gpurun_out/corrmfma_pmc_$TAG.json corr_mfma_i8 \
+        -- python3 scripts/tune/corr_mfma.py --only-probe --reps 8
+      step mixmfmapmc_$TAG 600 python -u scripts/tune/pmc_cmd.py gpurun_out/mixmfma_pmc_$TAG.json mixdecim_mfma_i8 \
+        -- python3 scripts/tune/mixdecim_mfma.py --only-probe --reps 8 ;;
     cpp) step cpp_$TAG 600 python -u -m pytest tests/test_dropin_cpp.py -m gpu -v --timeout 240 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

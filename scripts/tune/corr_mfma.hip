@@ -42,7 +42,9 @@
 //   built on the host, copied once per workgroup.  Energy: the inclusive
 //   prefix P of |x|^2 over the staged span (uint32 wrap), e_i = P[i] - P[i-1024].
 // * Grid.  Persistent, one 512-lane workgroup per CU (8 waves, 2 per SIMD),
-//   8192 outputs per workgroup tile.
+//   8192 outputs per workgroup tile.  (Two 256-lane workgroups per CU, 4096
+//   outputs each, measured level with one -- 0.8355 against 0.8384 ms -- and
+//   no longer fit with the bank-conflict-free B copies.)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -53,7 +55,10 @@ typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 namespace {
 constexpr int NP = 1024;                 // pattern length (config 5)
-constexpr int WAVES = 8;
+#ifndef CORR_WAVES
+#define CORR_WAVES 8                     // waves per workgroup (8: one workgroup per CU)
+#endif
+constexpr int WAVES = CORR_WAVES;
 constexpr int LANES = 64 * WAVES;
 constexpr int TILE = 1024 * WAVES;       // outputs per workgroup tile
 constexpr int SPAN = TILE + NP;          // staged samples per tile
@@ -61,14 +66,19 @@ constexpr int GROUPS = SPAN / 32;        // 32-sample groups
 constexpr int PLANE = GROUPS * 80;       // bytes per limb plane (64 B data + 16 B pad per group)
 constexpr int CHUNKS = (NP + 32) / 16;   // 66
 constexpr int BENT = 1096;               // entries per B copy (2 B each)
-constexpr int BSTRIDE = 2240;            // bytes per B copy
-constexpr int BKIND = 4 * BSTRIDE;       // 4 shifted copies per kind
+constexpr int BSTRIDE = 2 * BENT;        // bytes per B copy
+// copy sigma's base inside a kind: {0, 56, 120, 184} mod 256, so the 32 lanes of
+// a ds_read_b64 (8 lanes per copy, 64 contiguous bytes each) cover the 64 banks
+// exactly once (no bank conflicts; a uniform copy stride leaves 2-way ones)
+constexpr int BKIND = 7096 + BSTRIDE;    // 4 shifted copies per kind
 constexpr int BBYTES = 4 * BKIND;        // 4 kinds: re lo, re hi, im lo, im hi
 constexpr int LDS_A = 2 * PLANE;
 constexpr int LDS_P = SPAN * 4;
 constexpr int LDS_TOTAL = BBYTES + LDS_A + LDS_P + WAVES * 4;
-static_assert(SPAN % 32 == 0 && TILE % 8192 == 0, "tile shape");
-static_assert(LDS_TOTAL <= 160 * 1024, "LDS");
+constexpr int WG_PER_CU = 8 / WAVES;     // 2 waves per SIMD either way
+static_assert(2360 >= BSTRIDE && 4728 - 2360 >= BSTRIDE && 7096 - 4728 >= BSTRIDE, "B copies overlap");
+static_assert(SPAN % 32 == 0 && TILE % 1024 == 0, "tile shape");
+static_assert(WG_PER_CU * LDS_TOTAL <= 160 * 1024, "LDS");
 }  // namespace
 
 __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
@@ -76,7 +86,7 @@ __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
     return __builtin_amdgcn_perm(hi, lo, sel);
 }
 
-__global__ void __launch_bounds__(LANES, 1)
+__global__ void __launch_bounds__(LANES, WG_PER_CU)
 corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ btab, int cs, uint32_t bias_re,
              uint32_t bias_im, uint32_t* __restrict__ corr_out, uint32_t* __restrict__ e_out, long n_tiles,
              int store_all)
@@ -102,7 +112,8 @@ corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ bta
     const int a_base = 80 * (32 * w + rc) + 16 * h;
     // B: copy sigma = (col + 1) & 3, entry e = 16 t + 8 h - col + 31 + sigma (multiple of 4)
     const int sig = (rc + 1) & 3;
-    const int b_base = sig * BSTRIDE + 2 * (8 * h - rc + 31 + sig);
+    const int copy_off[4] = {0, 2360, 4728, 7096};
+    const int b_base = copy_off[sig] + 2 * (8 * h - rc + 31 + sig);
 
     // next tile's input, fetched into registers before the current tile's
     // MFMA work: granule g = tid + 512 k of the span; the buffer descriptor's
@@ -179,51 +190,70 @@ corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ bta
         }
         __syncthreads();
 
-        // ---- correlation: 66 chunks x 8 MFMAs into 6 accumulators
+        // ---- correlation: 66 chunks x 8 MFMAs into 6 accumulators; the next
+        // chunk's 6 fragments are read before the current chunk's MFMAs
         v16i s0r = {}, s1r = {}, s2r = {}, s0i = {}, s1i = {}, s2i = {};
         const unsigned char* pa = ldsA + a_base;
         const unsigned char* pb = ldsB + b_base;
+        struct Frags { v4i xl, xh, rl, rh, il, ih; };
+        auto load = [&](int t) {
+            Frags f;
+            const int ao = 80 * (t >> 1) + 32 * (t & 1);
+            f.xl = *(const v4i*)(pa + ao);
+            f.xh = *(const v4i*)(pa + PLANE + ao);
+            const int bo = 32 * t;
+            f.rl = *(const v4i*)(pb + bo);  // 8-B aligned: two b64 halves
+            f.rh = *(const v4i*)(pb + BKIND + bo);
+            f.il = *(const v4i*)(pb + 2 * BKIND + bo);
+            f.ih = *(const v4i*)(pb + 3 * BKIND + bo);
+            return f;
+        };
+        Frags cur = load(0);
 #pragma unroll 2
         for (int t = 0; t < CHUNKS; ++t) {
-            const int ao = 80 * (t >> 1) + 32 * (t & 1);
-            const v4i axl = *(const v4i*)(pa + ao);
-            const v4i axh = *(const v4i*)(pa + PLANE + ao);
-            const int bo = 32 * t;
-            v2i b0a = *(const v2i*)(pb + bo), b0b = *(const v2i*)(pb + bo + 8);
-            v2i b1a = *(const v2i*)(pb + BKIND + bo), b1b = *(const v2i*)(pb + BKIND + bo + 8);
-            v2i b2a = *(const v2i*)(pb + 2 * BKIND + bo), b2b = *(const v2i*)(pb + 2 * BKIND + bo + 8);
-            v2i b3a = *(const v2i*)(pb + 3 * BKIND + bo), b3b = *(const v2i*)(pb + 3 * BKIND + bo + 8);
-            const v4i brl = {b0a[0], b0a[1], b0b[0], b0b[1]};
-            const v4i brh = {b1a[0], b1a[1], b1b[0], b1b[1]};
-            const v4i bil = {b2a[0], b2a[1], b2b[0], b2b[1]};
-            const v4i bih = {b3a[0], b3a[1], b3b[0], b3b[1]};
-            s0r = __builtin_amdgcn_mfma_i32_32x32x32_i8(axl, brl, s0r, 0, 0, 0);
-            s0i = __builtin_amdgcn_mfma_i32_32x32x32_i8(axl, bil, s0i, 0, 0, 0);
-            s1r = __builtin_amdgcn_mfma_i32_32x32x32_i8(axl, brh, s1r, 0, 0, 0);
-            s1i = __builtin_amdgcn_mfma_i32_32x32x32_i8(axl, bih, s1i, 0, 0, 0);
-            s1r = __builtin_amdgcn_mfma_i32_32x32x32_i8(axh, brl, s1r, 0, 0, 0);
-            s1i = __builtin_amdgcn_mfma_i32_32x32x32_i8(axh, bil, s1i, 0, 0, 0);
-            s2r = __builtin_amdgcn_mfma_i32_32x32x32_i8(axh, brh, s2r, 0, 0, 0);
-            s2i = __builtin_amdgcn_mfma_i32_32x32x32_i8(axh, bih, s2i, 0, 0, 0);
+            const Frags nxt = load(t + 1 < CHUNKS ? t + 1 : t);
+            s0r = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl, cur.rl, s0r, 0, 0, 0);
+            s0i = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl, cur.il, s0i, 0, 0, 0);
+            s1r = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl, cur.rh, s1r, 0, 0, 0);
+            s1i = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl, cur.ih, s1i, 0, 0, 0);
+            s1r = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh, cur.rl, s1r, 0, 0, 0);
+            s1i = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh, cur.il, s1i, 0, 0, 0);
+            s2r = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh, cur.rh, s2r, 0, 0, 0);
+            s2i = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh, cur.ih, s2i, 0, 0, 0);
+            cur = nxt;
         }
 
-        // ---- epilogue: D layout col = l & 31, row = (r & 3) + 8 (r >> 2) + 4 h
+        // ---- epilogue: D layout col = l & 15.. 31, row = (r & 3) + 8 (r >> 2) + 4 h
         const unsigned es = (unsigned)(cs / 2) & 31u;
+        const long iw = i0 + 1024 * w;
+        const bool full = iw + 1024 <= n;
+        uint32_t* co = corr_out + iw;
+        uint32_t* eo = e_out + iw;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-            const long i = i0 + 1024 * w + 32 * row + rc;
+            const int o = 32 * row + rc;  // output iw + o
             const uint32_t cr = (uint32_t)s0r[r] + ((uint32_t)s1r[r] << 8) + ((uint32_t)s2r[r] << 16) + bias_re;
             const uint32_t ci = (uint32_t)s0i[r] + ((uint32_t)s1i[r] << 8) + ((uint32_t)s2i[r] << 16) + bias_im;
-            const int32_t tr = ((int32_t)cr >> (cs & 31)) >> 2;  // scale32 (dsp_complex.cpp:43-46), then :250
-            const int32_t ti = ((int32_t)ci >> (cs & 31)) >> 2;
-            const uint32_t corr = (uint32_t)tr * (uint32_t)tr + (uint32_t)ti * (uint32_t)ti;
-            // local sample index of output i: i - j0; window (i - 1024, i]
-            const int li = 1024 * w + 32 * row + rc + NP;
+            // scale32 (dsp_complex.cpp:43-46), then :250; |t| < 2^22 for cs >= 7 (host check), so the
+            // 24-bit multiplier gives the wrapped int32 squares
+            // (the shift pair as one arithmetic shift by cs + 2; the sign extension from 24 bits is
+            // exact here and lets the compiler use v_mul_i32_i24)
+            const int sh = (cs & 31) + 2;
+            const int32_t tr = (((int32_t)cr >> sh) << 8) >> 8;
+            const int32_t ti = (((int32_t)ci >> sh) << 8) >> 8;
+            const uint32_t corr = (uint32_t)(tr * tr) + (uint32_t)(ti * ti);
+            // local sample index of output iw + o is 1024 w + o + NP; window (li - 1024, li]
+            const int li = 1024 * w + o + NP;
             const uint32_t e = (ldsP[li] - ldsP[li - NP]) >> es;
-            if (i < n && (store_all || (corr == 0xFFFFFFFFu && e == 0xFFFFFFFFu))) {
-                corr_out[i] = corr;
-                e_out[i] = e;
+            if (store_all) {
+                if (full || iw + o < n) {
+                    co[o] = corr;
+                    eo[o] = e;
+                }
+            } else if ((corr & e) == 0xFFFFFFFFu) {  // never (keeps the work live for timing)
+                co[o] = corr;
+                eo[o] = e;
             }
         }
     }
@@ -250,7 +280,8 @@ extern "C" int tune_corr_mfma(const void* x, long n, const void* btab, int cs, u
     }
     const long n_tiles = (n + TILE - 1) / TILE;
     if (n % 4 != 0 || 4 * n >= (1l << 31)) return 1;  // granule loads and the wrapped-offset zero fill
-    if (grid <= 0) grid = 256;
+    if (cs < 7 || cs > 29) return 2;                      // the epilogue's shift by cs + 2 and 24-bit squares
+    if (grid <= 0) grid = 256 * WG_PER_CU;
     if (grid > n_tiles) grid = (int)n_tiles;
     hipLaunchKernelGGL(corr_mfma_i8, dim3(grid), dim3(LANES), LDS_TOTAL, s, (const uint32_t*)x, n,
                        (const v4u*)btab, cs, bias_re, bias_im, (uint32_t*)corr_out, (uint32_t*)e_out, n_tiles,

@@ -38,8 +38,9 @@ from srcdsp_amd.design import qpsk_pattern  # noqa: E402
 
 NP = 1024
 CHUNKS = 66
-BENT, BSTRIDE = 1096, 2240
-BKIND = 4 * BSTRIDE
+BENT, BSTRIDE = 1096, 2192  # corr_mfma.hip's B copy geometry (checked against the library at run time)
+COPY_OFF = (0, 2360, 4728, 7096)  # copy sigma's base in a kind: {0, 56, 120, 184} mod 256 (bank-conflict free)
+BKIND = COPY_OFF[3] + BSTRIDE
 I8_PEAK = 1024 * 1024 * 2.4e9    # MACs/s: 1024 SIMDs x 1024 i8 MACs per clock (32x32x32 in 32 cycles)
 DOT2_PEAK = 39.32e12             # v_dot2 lane-ops/s (bench.py VALU_PEAK_TOPS)
 
@@ -78,7 +79,7 @@ def btables(p):
         v = (lo if limb == 0 else hi).view(np.uint8)  # (1024, 2)
         bias[out] = int((128 * pairs[out].sum()) % (1 << 32))
         for sig in range(4):
-            base = ki * BKIND + sig * BSTRIDE
+            base = ki * BKIND + COPY_OFF[sig]
             e = np.arange(BENT)
             k = e - sig - 32
             ok = (k >= 0) & (k < NP)
@@ -143,7 +144,7 @@ def emulate(p, x, n_out):
                 for col in range(32):
                     sig = (col + 1) & 3
                     for h in range(2):
-                        addr = ki * BKIND + sig * BSTRIDE + 2 * (8 * h - col + 31 + sig) + 32 * t
+                        addr = ki * BKIND + COPY_OFF[sig] + 2 * (8 * h - col + 31 + sig) + 32 * t
                         assert addr % 8 == 0
                         b[col, h] = kinds[addr:addr + 16]
                 B[nm] = b
@@ -165,7 +166,10 @@ def emulate(p, x, n_out):
 
 def run_gpu(args, p, x):
     import torch
-    lib = C.CDLL(os.path.join(HERE, "libcorrmfma.so"))
+    lib = C.CDLL(os.path.join(HERE, args.lib))
+    geo = (C.c_int * 8)()
+    lib.tune_corr_mfma_geometry(geo)
+    assert (geo[1], geo[2], geo[3], geo[4]) == (CHUNKS, BENT, BSTRIDE, BKIND), list(geo)
     lib.tune_corr_mfma.argtypes = [C.c_void_p, C.c_long, C.c_void_p, C.c_int, C.c_uint32, C.c_uint32, C.c_void_p,
                                    C.c_void_p, C.c_int, C.c_int, C.c_void_p]
     img, bias = btables(p)
@@ -183,7 +187,12 @@ def run_gpu(args, p, x):
                                 C.c_void_p(st.cuda_stream))
         assert rc == 0, rc
 
-    out = {"samples": n, "coeff_scaling": cs, "bias": bias}
+    out = {"samples": n, "coeff_scaling": cs, "bias": bias, "lib": args.lib, "tile": geo[0], "lds": geo[7]}
+    if args.only_probe:  # counter passes: the probe's launches alone
+        for _ in range(args.reps):
+            launch(0)
+        torch.cuda.synchronize()
+        return
     launch(1)
     torch.cuda.synchronize()
     got_c = dc.cpu().numpy().view(np.uint32)
@@ -246,10 +255,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--samples", type=int, default=1 << 26)
     ap.add_argument("--emulate", type=int, default=0)
-    ap.add_argument("--grid", type=int, default=256)
+    ap.add_argument("--grid", type=int, default=0, help="0: 256 x workgroups per CU")
+    ap.add_argument("--lib", default="libcorrmfma.so", help="probe library (tuning builds of corr_mfma.hip)")
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--only-probe", action="store_true", help="launch the probe --reps times, nothing else")
     args = ap.parse_args()
     p, x = config5_buffer(args.samples)
     if args.emulate:

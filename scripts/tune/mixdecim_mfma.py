@@ -1,0 +1,226 @@
+#!/usr/bin/env python3
+"""Config 4's tap loop on the integer matrix cores (tuning probe, VERDICT r5
+item 4; the kernel is scripts/tune/mixdecim_mfma.hip and never ships).
+
+1. Config 4's input (2^28 complex<int16_t>, the bench's synthetic generator),
+   the 127 Q14 taps and the Mixer<ci16,ci16,int16_t,4096> table at f = 0.1
+   (the oracle's table and phase words, mixers.h:51-67 / :155-158).
+2. Runs the probe and compares EVERY one of the 2^26 outputs with the oracle
+   (the oracle mixer over the whole call, then the oracle decimator in parallel
+   windows, as tests/test_gpu_parity.py's test_config4_whole_output) and with
+   the product's fused chain on the same device input.
+3. Times the probe and the product chain on the same box (HIP events), and
+   reports both against the HBM bound (5 B per input sample) and the probe's
+   MFMA share.
+
+--emulate N: no GPU; numpy replay of the kernel's fragments (B tables, lane
+addresses, limb planes) for the first N input samples against the oracle."""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+    sys.path.insert(0, p)
+
+import pyoracle  # noqa: E402
+from srcdsp_amd.design import hamming_sinc, q14  # noqa: E402
+
+SEED = 0x5EED
+I8_PEAK = 1024 * 1024 * 2.4e9  # MACs/s (16x16x64 i8: 16 cycles per SIMD)
+HBM = 8.0e12
+
+
+def limbs(v):
+    v = np.asarray(v, np.int64)
+    vl = ((v + 128) & 255) - 128
+    vh = (v - vl) >> 8
+    assert vh.min() >= -128 and vh.max() <= 127
+    return vl, vh
+
+
+def bfrags(c):
+    """[6 fragments f = 2 t + limb][64 lanes][16 bytes]: lane (col = l & 15,
+    h = l >> 4), byte j: limb of c[4 col - base_t - (16 h + j)], base_t =
+    -128 + 64 t, zero outside [0, 126]."""
+    cl, ch = limbs(c)
+    out = np.zeros((6, 64, 16), np.int8)
+    for t in range(3):
+        base = -128 + 64 * t
+        for lane in range(64):
+            col, h = lane & 15, lane >> 4
+            k = 4 * col - base - (16 * h + np.arange(16))
+            ok = (k >= 0) & (k < len(c))
+            out[2 * t, lane, ok] = cl[k[ok]]
+            out[2 * t + 1, lane, ok] = ch[k[ok]]
+    return out
+
+
+def mixer_words(f=0.1, N=4096):
+    o = pyoracle.Oracle(0)
+    m = o.mixer(N)
+    m.reset(f)
+    T = m.table().astype(np.int64)
+    phase, freq, _ = m.state()
+    phi = np.arange(N)
+    cos, sin = T[(phi + N // 4) % N], T[phi]
+    A = (cos & 0xFFFF) | ((-sin & 0xFFFF) << 16)
+    B = (sin & 0xFFFF) | ((cos & 0xFFFF) << 16)
+    return np.stack([A, B], 1).astype(np.uint32), phase, freq
+
+
+def oracle_chain(x, c, f=0.1):
+    import fullsize as F
+    o = pyoracle.Oracle(0)
+    m = o.mixer(4096)
+    m.reset(f)
+    mixed = m.step(x)
+    return F.decim_all(lambda: o.decim(1, 4, c), mixed, 4, 128, np.empty((len(x) // 4, 2), np.int16))
+
+
+def emulate(x, c, n):
+    """numpy replay of mixdecim_mfma_i8's fragment algebra for n inputs."""
+    tab, phi0, freq = mixer_words()
+    bias = int(128 * np.asarray(c, np.int64).sum()) % (1 << 32)
+    bf = bfrags(c).astype(np.int64)
+    o = pyoracle.Oracle(0)
+    mx = o.mixer(4096)
+    mx.reset(0.1)
+    m = np.zeros((n + 128, 2), np.int64)
+    m[128:] = mx.step(x[:n]).astype(np.int64)
+    ml = (m & 255) - 128
+    mh = m >> 8
+    y = np.zeros((n // 4, 2), np.int64)
+    for wt in range(n // 512):
+        acc = np.zeros((3, 16, 16), np.int64)  # S0..S2 [row][col]
+        for t in range(3):
+            A = {}
+            for nm, pl in (("l", ml), ("h", mh)):
+                a = np.zeros((16, 4, 16), np.int64)
+                for row in range(16):
+                    for h in range(4):
+                        s0 = 128 + 512 * wt + 64 * (row >> 1) - 128 + 16 * h + 64 * t
+                        a[row, h] = pl[s0:s0 + 16, row & 1]
+                A[nm] = a
+            b = {lim: bf[2 * t + lim].reshape(4, 16, 16).transpose(1, 0, 2) for lim in (0, 1)}  # [col][h][j]
+
+            def mm(a, bb):
+                return np.einsum("rhj,chj->rc", a, bb)
+            acc[0] += mm(A["l"], b[0])
+            acc[1] += mm(A["l"], b[1]) + mm(A["h"], b[0])
+            acc[2] += mm(A["h"], b[1])
+        tot = (acc[0] + (acc[1] << 8) + (acc[2] << 16) + bias) & 0xFFFFFFFF
+        v = tot.astype(np.uint32).view(np.int32).astype(np.int64) >> 14
+        v = np.clip(v, -32767, 32767)
+        for row in range(16):
+            blk, comp = row >> 1, row & 1
+            y[128 * wt + 16 * blk:128 * wt + 16 * blk + 16, comp] = v[row]
+    return y.astype(np.int16)
+
+
+def run_gpu(args, x, c):
+    import torch
+    import srcdsp_amd as S
+    lib = C.CDLL(os.path.join(HERE, "libmixdecimmfma.so"))
+    lib.tune_mixdecim_mfma.argtypes = [C.c_void_p, C.c_long, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                       C.c_uint32, C.c_void_p, C.c_int, C.c_void_p]
+    tab, phi0, freq = mixer_words()
+    bias = int(128 * np.asarray(c, np.int64).sum()) % (1 << 32)
+    n = args.samples
+    dx = torch.empty((n, 2), dtype=torch.int16, device="cuda")
+    S.fill_synthetic(dx, "ci16", seed=SEED, channel=0, lo=-8192, hi=8191)
+    db = torch.from_numpy(bfrags(c).reshape(-1).view(np.uint8)).cuda()
+    dt = torch.from_numpy(tab).cuda()
+    dy = torch.zeros((n // 4, 2), dtype=torch.int16, device="cuda")
+    st = torch.cuda.current_stream()
+
+    def launch():
+        rc = lib.tune_mixdecim_mfma(C.c_void_p(dx.data_ptr()), n, C.c_void_p(db.data_ptr()),
+                                    C.c_void_p(dt.data_ptr()), phi0, freq, bias, C.c_void_p(dy.data_ptr()),
+                                    args.grid, C.c_void_p(st.cuda_stream))
+        assert rc == 0, rc
+
+    m = S.Mixer(4096)
+    m.reset(0.1)
+    d = S.FilterDnsamplingFir(c, 4, "complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int32_t")
+    chain = S.MixerDecimatorChain(m, d)
+    dyp = torch.empty_like(dy)
+
+    def prod():  # the first call is the fresh chain (checked); later ones continue the stream (same work)
+        chain.step(dx, dyp)
+
+    out = {"samples": n, "phi0": phi0, "freq": freq, "bias": bias}
+    if args.only_probe:  # counter passes: the probe's launches alone
+        for _ in range(args.reps):
+            launch()
+        torch.cuda.synchronize()
+        return
+    launch()
+    prod()
+    torch.cuda.synchronize()
+    got = dy.cpu().numpy()
+    out["probe_vs_product_mismatches"] = int((got != dyp.cpu().numpy()).any(axis=1).sum())
+    if not args.no_check:
+        import fullsize as F
+        want = oracle_chain(dx.cpu().numpy(), c)
+        bad = F.first_bad(got, want)
+        out["probe_vs_oracle_first_bad"] = bad
+        out["outputs_checked"] = int(len(want))
+    print(json.dumps({"check": out}), flush=True)
+
+    def timeit(fn, reps):
+        for _ in range(args.warmup):
+            fn()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for a, b in ev:
+            a.record(st)
+            fn()
+            b.record(st)
+        torch.cuda.synchronize()
+        return [a.elapsed_time(b) for a, b in ev]
+
+    res = {}
+    for rnd in range(args.rounds):  # interleaved rounds, same box
+        for nm, fn in (("probe", launch), ("product", prod)):
+            ms = timeit(fn, args.reps)
+            res.setdefault(nm, []).append(float(np.mean(ms)))
+    macs = n / 512 * 12 * 16384  # 12 MFMAs of 16384 MACs per 512 input samples
+    for nm, v in res.items():
+        t = min(v) * 1e-3
+        out[nm] = {"ms_rounds": [round(q, 4) for q in v], "gsamples_per_s": round(n / t / 1e9, 2),
+                   "hbm_frac_5B": round(5.0 * n / t / HBM, 4)}
+    out["probe"]["i8_peak_frac"] = round(macs / (min(res["probe"]) * 1e-3) / I8_PEAK, 4)
+    out["speedup"] = round(min(res["product"]) / min(res["probe"]), 3)
+    print(json.dumps(out), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--samples", type=int, default=1 << 28)
+    ap.add_argument("--emulate", type=int, default=0)
+    ap.add_argument("--grid", type=int, default=512)
+    ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--only-probe", action="store_true", help="launch the probe --reps times, nothing else")
+    args = ap.parse_args()
+    c = q14(hamming_sinc(127))
+    if args.emulate:
+        n = args.emulate
+        x = pyoracle.Oracle(0).gen_ci16(SEED, 0, 0, n, -8192, 8191)
+        got = emulate(x, c, n)
+        want = oracle_chain(x, c)
+        bad = np.nonzero((got != want).any(axis=1))[0]
+        print(f"emulate: {len(want)} outputs, {len(bad)} differ from the oracle" + (f" (first {bad[0]})" if len(bad) else ""))
+        sys.exit(1 if len(bad) else 0)
+    run_gpu(args, None, c)
+
+
+if __name__ == "__main__":
+    main()
