@@ -27,7 +27,7 @@
 #   dist             the 2-rank GPU test of the N > 1 path (tests/test_gpu_dist.py)
 #   cpp              the drop-in C++ tests (tests/test_dropin_cpp.py -m gpu)
 #   mfma             the integer matrix-core probes (tuning only, never shipped): config 5's correlator
-#                    (scripts/tune/corr_mfma.py ${CORR_ARGS}) and config 4's tap loop
+#                    (scripts/tune/corr_mfma.py ${CORR_ARGS}, for each of ${CORR_LIBS}) and config 4's tap loop
 #                    (scripts/tune/mixdecim_mfma.py ${MIX_ARGS}), each checked against the oracle and timed
 #                    beside the product on the same box
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -95,11 +95,15 @@ for s in ${STEPS:-smoke tests bench}; do
     ab) step ab_$TAG 1000 bash scripts/tune/ab_libs.sh ;;
     dist) step dist_$TAG 300 python -u -m pytest tests/test_gpu_dist.py -m gpu -v --timeout 240 --timeout-method thread ;;
     mfma)
-      step corrmfma_$TAG 400 python -u scripts/tune/corr_mfma.py ${CORR_ARGS}
+      for lib in ${CORR_LIBS:-libcorrmfma.so}; do
+        step corrmfma_${lib%.so}_$TAG 400 python -u scripts/tune/corr_mfma.py --lib $lib ${CORR_ARGS}
+      done
       step mixmfma_$TAG 400 python -u scripts/tune/mixdecim_mfma.py ${MIX_ARGS} ;;
     mfmapmc)  # SQ / MFMA counter passes of the two probes' kernels
-      step corrmfmapmc_$TAG 600 python -u scripts/tune/pmc_cmd.py gpurun_out/corrmfma_pmc_$TAG.json corr_mfma_i8 \
-        -- python3 scripts/tune/corr_mfma.py --only-probe --reps 8
+      for lib in ${CORR_LIBS:-libcorrmfma.so}; do
+        step corrmfmapmc_${lib%.so}_$TAG 600 python -u scripts/tune/pmc_cmd.py gpurun_out/corrmfma_pmc_${lib%.so}_$TAG.json \
+          corr_mfma_i8 -- python3 scripts/tune/corr_mfma.py --only-probe --reps 8 --lib $lib
+      done
       step mixmfmapmc_$TAG 600 python -u scripts/tune/pmc_cmd.py gpurun_out/mixmfma_pmc_$TAG.json mixdecim_mfma_i8 \
         -- python3 scripts/tune/mixdecim_mfma.py --only-probe --reps 8 ;;
     cpp) step cpp_$TAG 600 python -u -m pytest tests/test_dropin_cpp.py -m gpu -v --timeout 240 --timeout-method thread ;;

@@ -35,9 +35,11 @@
 //   in the same byte order for A and B (scripts/tune/mfma_i8_probe.py checks
 //   that the instruction sums A byte j of lane (r, h) with B byte j of lane
 //   (c, h) for every j and h).
-// * LDS.  A: two byte planes (xl, xh), (re, im) per sample, 16 B pad per 32
-//   samples (row stride 80 B: the 16 lanes of a ds_read_b128 quarter hit 16
-//   different bank quads).  B: per kind, 4 copies of the limb array shifted by
+// * LDS.  A: two byte planes (xl, xh), (re, im) per sample, 64 B per 32
+//   samples with the four 16-B slots of a group XOR-swizzled by bits 2-3 of
+//   the group index (the 16 lanes of a ds_read_b128 quarter, 16 consecutive
+//   groups, hit 16 different bank quads; round 6's first version padded each
+//   group to 80 B instead).  B: per kind, 4 copies of the limb array shifted by
 //   0..3 entries so every lane's 8 entries start 8-B aligned (2 ds_read_b64);
 //   built on the host, copied once per workgroup.  Energy: the inclusive
 //   prefix P of |x|^2 over the staged span (uint32 wrap), e_i = P[i] - P[i-1024].
@@ -63,7 +65,7 @@ constexpr int LANES = 64 * WAVES;
 constexpr int TILE = 1024 * WAVES;       // outputs per workgroup tile
 constexpr int SPAN = TILE + NP;          // staged samples per tile
 constexpr int GROUPS = SPAN / 32;        // 32-sample groups
-constexpr int PLANE = GROUPS * 80;       // bytes per limb plane (64 B data + 16 B pad per group)
+constexpr int PLANE = GROUPS * 64;       // bytes per limb plane (64 B per 32-sample group, swizzled)
 constexpr int CHUNKS = (NP + 32) / 16;   // 66
 constexpr int BENT = 1096;               // entries per B copy (2 B each)
 constexpr int BSTRIDE = 2 * BENT;        // bytes per B copy
@@ -71,30 +73,46 @@ constexpr int BSTRIDE = 2 * BENT;        // bytes per B copy
 // a ds_read_b64 (8 lanes per copy, 64 contiguous bytes each) cover the 64 banks
 // exactly once (no bank conflicts; a uniform copy stride leaves 2-way ones)
 constexpr int BKIND = 7096 + BSTRIDE;    // 4 shifted copies per kind
-constexpr int BBYTES = 4 * BKIND;        // 4 kinds: re lo, re hi, im lo, im hi
+// B kinds: 2 pattern limbs -> re lo, re hi, im lo, im hi; 1 limb -> re, im
+template <int PL> constexpr int BBYTES = 2 * PL * BKIND;
 constexpr int LDS_A = 2 * PLANE;
 constexpr int LDS_P = SPAN * 4;
-constexpr int LDS_TOTAL = BBYTES + LDS_A + LDS_P + WAVES * 4;
+template <int PL> constexpr int LDS_TOTAL = BBYTES<PL> + LDS_A + LDS_P + WAVES * 4;
 constexpr int WG_PER_CU = 8 / WAVES;     // 2 waves per SIMD either way
 static_assert(2360 >= BSTRIDE && 4728 - 2360 >= BSTRIDE && 7096 - 4728 >= BSTRIDE, "B copies overlap");
 static_assert(SPAN % 32 == 0 && TILE % 1024 == 0, "tile shape");
-static_assert(WG_PER_CU * LDS_TOTAL <= 160 * 1024, "LDS");
+static_assert(WG_PER_CU * LDS_TOTAL<2> <= 160 * 1024, "LDS");
 }  // namespace
+
+// byte address of staged sample js in a limb plane: group js >> 5 (64 B), its
+// 16-B slot (js >> 3) & 3 XOR-swizzled by bits 2-3 of the group, 2 B per sample
+__device__ __forceinline__ int sample_addr(int js)
+{
+    const int g = js >> 5;
+    return 64 * g + 16 * (((js >> 3) & 3) ^ ((g >> 2) & 3)) + 2 * (js & 7);
+}
 
 __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
 {
     return __builtin_amdgcn_perm(hi, lo, sel);
 }
 
+// PL = 2: any pattern with |component| < 32640 (two limbs, S0..S2 per
+// component, 8 MFMAs per chunk).  PL = 1: pattern = scale * q with every q
+// component in [-128, 127] (the host factors out the gcd of the components,
+// e.g. 500 for config 5's +-500 QPSK pattern): one limb, S0 = xl.q,
+// S1 = xh.q, 4 MFMAs per chunk, C = scale (S0 + (S1 << 8) + bias) mod 2^32
+// (exact: C = sum x (scale q) = scale sum x q in Z/2^32).
+template <int PL>
 __global__ void __launch_bounds__(LANES, WG_PER_CU)
 corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ btab, int cs, uint32_t bias_re,
-             uint32_t bias_im, uint32_t* __restrict__ corr_out, uint32_t* __restrict__ e_out, long n_tiles,
-             int store_all)
+             uint32_t bias_im, uint32_t scale, uint32_t* __restrict__ corr_out, uint32_t* __restrict__ e_out,
+             long n_tiles, int store_all)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     unsigned char* ldsB = lds;
-    unsigned char* ldsA = lds + BBYTES;                 // xl plane, then xh plane
-    uint32_t* ldsP = (uint32_t*)(lds + BBYTES + LDS_A);  // prefix of |x|^2
+    unsigned char* ldsA = lds + BBYTES<PL>;                 // xl plane, then xh plane
+    uint32_t* ldsP = (uint32_t*)(lds + BBYTES<PL> + LDS_A);  // prefix of |x|^2
     uint32_t* ldsW = ldsP + SPAN;                        // per-wave totals of the scan
 
     const int tid = threadIdx.x;
@@ -104,12 +122,14 @@ corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ bta
     const int rc = lane & 31;  // A row / B col / D col
 
     // B tables, once per workgroup
-    for (int i = tid; i < BBYTES / 16; i += LANES)
+    for (int i = tid; i < BBYTES<PL> / 16; i += LANES)
         ((v4u*)ldsB)[i] = btab[i];
 
     // per-lane LDS bases
-    // A: group 32 w + row (+ t >> 1), byte 32 (t & 1) + 16 h
-    const int a_base = 80 * (32 * w + rc) + 16 * h;
+    // A: group g = 32 w + row + (t >> 1), 16-B slot 2 (t & 1) + h of it, stored
+    // at slot ^ ((g >> 2) & 3) (sample_addr): 16 consecutive rows are 16
+    // consecutive groups, so a ds_read_b128 quarter hits 16 bank quads
+    const int a_g0 = 32 * w + rc;
     // B: copy sigma = (col + 1) & 3, entry e = 16 t + 8 h - col + 31 + sigma (multiple of 4)
     const int sig = (rc + 1) & 3;
     const int copy_off[4] = {0, 2360, 4728, 7096};
@@ -145,7 +165,7 @@ corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ bta
             if (g >= SPAN / 4) break;
             const v4u v = pre[k];
             const int js = 4 * g;
-            const int off = 80 * (js >> 5) + 2 * (js & 31);
+            const int off = sample_addr(js);
             uint32_t lo0 = perm(v[1], v[0], 0x06040200u) ^ 0x80808080u;
             uint32_t lo1 = perm(v[3], v[2], 0x06040200u) ^ 0x80808080u;
             uint32_t hi0 = perm(v[1], v[0], 0x07050301u);
@@ -190,22 +210,27 @@ corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ bta
         }
         __syncthreads();
 
-        // ---- correlation: 66 chunks x 8 MFMAs into 6 accumulators; the next
-        // chunk's 6 fragments are read before the current chunk's MFMAs
+        // ---- correlation: 66 chunks x 8 (PL = 2) or 4 (PL = 1) MFMAs; the
+        // next chunk's fragments are read before the current chunk's MFMAs
         v16i s0r = {}, s1r = {}, s2r = {}, s0i = {}, s1i = {}, s2i = {};
-        const unsigned char* pa = ldsA + a_base;
+        const unsigned char* pa = ldsA;
         const unsigned char* pb = ldsB + b_base;
         struct Frags { v4i xl, xh, rl, rh, il, ih; };
         auto load = [&](int t) {
             Frags f;
-            const int ao = 80 * (t >> 1) + 32 * (t & 1);
+            const int g = a_g0 + (t >> 1);
+            const int ao = 64 * g + 16 * ((2 * (t & 1) + h) ^ ((g >> 2) & 3));
             f.xl = *(const v4i*)(pa + ao);
             f.xh = *(const v4i*)(pa + PLANE + ao);
             const int bo = 32 * t;
             f.rl = *(const v4i*)(pb + bo);  // 8-B aligned: two b64 halves
-            f.rh = *(const v4i*)(pb + BKIND + bo);
-            f.il = *(const v4i*)(pb + 2 * BKIND + bo);
-            f.ih = *(const v4i*)(pb + 3 * BKIND + bo);
+            if constexpr (PL == 2) {
+                f.rh = *(const v4i*)(pb + BKIND + bo);
+                f.il = *(const v4i*)(pb + 2 * BKIND + bo);
+                f.ih = *(const v4i*)(pb + 3 * BKIND + bo);
+            } else {
+                f.il = *(const v4i*)(pb + BKIND + bo);
+            }
             return f;
         };
         Frags cur = load(0);
@@ -214,12 +239,14 @@ corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ bta
             const Frags nxt = load(t + 1 < CHUNKS ? t + 1 : t);
             s0r = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl, cur.rl, s0r, 0, 0, 0);
             s0i = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl, cur.il, s0i, 0, 0, 0);
-            s1r = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl, cur.rh, s1r, 0, 0, 0);
-            s1i = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl, cur.ih, s1i, 0, 0, 0);
+            if constexpr (PL == 2) {
+                s1r = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl, cur.rh, s1r, 0, 0, 0);
+                s1i = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl, cur.ih, s1i, 0, 0, 0);
+                s2r = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh, cur.rh, s2r, 0, 0, 0);
+                s2i = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh, cur.ih, s2i, 0, 0, 0);
+            }
             s1r = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh, cur.rl, s1r, 0, 0, 0);
             s1i = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh, cur.il, s1i, 0, 0, 0);
-            s2r = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh, cur.rh, s2r, 0, 0, 0);
-            s2i = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh, cur.ih, s2i, 0, 0, 0);
             cur = nxt;
         }
 
@@ -233,8 +260,14 @@ corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ bta
         for (int r = 0; r < 16; ++r) {
             const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
             const int o = 32 * row + rc;  // output iw + o
-            const uint32_t cr = (uint32_t)s0r[r] + ((uint32_t)s1r[r] << 8) + ((uint32_t)s2r[r] << 16) + bias_re;
-            const uint32_t ci = (uint32_t)s0i[r] + ((uint32_t)s1i[r] << 8) + ((uint32_t)s2i[r] << 16) + bias_im;
+            uint32_t cr, ci;
+            if constexpr (PL == 2) {
+                cr = (uint32_t)s0r[r] + ((uint32_t)s1r[r] << 8) + ((uint32_t)s2r[r] << 16) + bias_re;
+                ci = (uint32_t)s0i[r] + ((uint32_t)s1i[r] << 8) + ((uint32_t)s2i[r] << 16) + bias_im;
+            } else {
+                cr = scale * ((uint32_t)s0r[r] + ((uint32_t)s1r[r] << 8) + bias_re);
+                ci = scale * ((uint32_t)s0i[r] + ((uint32_t)s1i[r] << 8) + bias_im);
+            }
             // scale32 (dsp_complex.cpp:43-46), then :250; |t| < 2^22 for cs >= 7 (host check), so the
             // 24-bit multiplier gives the wrapped int32 squares
             // (the shift pair as one arithmetic shift by cs + 2; the sign extension from 24 bits is
@@ -259,22 +292,21 @@ corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ bta
     }
 }
 
-extern "C" int tune_corr_mfma_lds_bytes() { return LDS_TOTAL; }
-extern "C" int tune_corr_mfma_btab_bytes() { return BBYTES; }
 extern "C" int tune_corr_mfma_geometry(int* out)
 {
-    out[0] = TILE; out[1] = CHUNKS; out[2] = BENT; out[3] = BSTRIDE; out[4] = BKIND; out[5] = BBYTES;
-    out[6] = PLANE; out[7] = LDS_TOTAL;
+    out[0] = TILE; out[1] = CHUNKS; out[2] = BENT; out[3] = BSTRIDE; out[4] = BKIND; out[5] = BBYTES<2>;
+    out[6] = PLANE; out[7] = LDS_TOTAL<2>;
     return 0;
 }
 
-extern "C" int tune_corr_mfma(const void* x, long n, const void* btab, int cs, uint32_t bias_re, uint32_t bias_im,
-                              void* corr_out, void* e_out, int grid, int store_all, hipStream_t s)
+template <int PL>
+static int launch(const void* x, long n, const void* btab, int cs, uint32_t bias_re, uint32_t bias_im,
+                  uint32_t scale, void* corr_out, void* e_out, int grid, int store_all, hipStream_t s)
 {
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)corr_mfma_i8, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           LDS_TOTAL);
+        hipError_t e = hipFuncSetAttribute((const void*)corr_mfma_i8<PL>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, LDS_TOTAL<PL>);
         if (e != hipSuccess) return (int)e;
         attr = true;
     }
@@ -283,8 +315,19 @@ extern "C" int tune_corr_mfma(const void* x, long n, const void* btab, int cs, u
     if (cs < 7 || cs > 29) return 2;                      // the epilogue's shift by cs + 2 and 24-bit squares
     if (grid <= 0) grid = 256 * WG_PER_CU;
     if (grid > n_tiles) grid = (int)n_tiles;
-    hipLaunchKernelGGL(corr_mfma_i8, dim3(grid), dim3(LANES), LDS_TOTAL, s, (const uint32_t*)x, n,
-                       (const v4u*)btab, cs, bias_re, bias_im, (uint32_t*)corr_out, (uint32_t*)e_out, n_tiles,
-                       store_all);
+    hipLaunchKernelGGL(corr_mfma_i8<PL>, dim3(grid), dim3(LANES), LDS_TOTAL<PL>, s, (const uint32_t*)x, n,
+                       (const v4u*)btab, cs, bias_re, bias_im, scale, (uint32_t*)corr_out, (uint32_t*)e_out,
+                       n_tiles, store_all);
     return (int)hipGetLastError();
+}
+
+// pattern_limbs 2: btab = 4 kinds, scale unused; 1: btab = 2 kinds of the
+// pattern divided by `scale`, biases of that quotient pattern
+extern "C" int tune_corr_mfma(const void* x, long n, const void* btab, int cs, uint32_t bias_re, uint32_t bias_im,
+                              void* corr_out, void* e_out, int grid, int store_all, int pattern_limbs, uint32_t scale,
+                              hipStream_t s)
+{
+    if (pattern_limbs == 1)
+        return launch<1>(x, n, btab, cs, bias_re, bias_im, scale, corr_out, e_out, grid, store_all, s);
+    return launch<2>(x, n, btab, cs, bias_re, bias_im, 1u, corr_out, e_out, grid, store_all, s);
 }

@@ -64,19 +64,41 @@ def limbs(v):
     return vl.astype(np.int8), vh.astype(np.int8)
 
 
-def btables(p):
-    """The kernel's LDS B image: 4 kinds (re lo, re hi, im lo, im hi) x 4
-    copies shifted by sigma; copy sigma entry e holds the coefficient pair of
-    tap k = e - sigma - 32 (zero outside [0, 1023]); pair = (comp 0, comp 1) =
-    re output: (c.re, -c.im) = (p.re, p.im); im output: (c.im, c.re) =
-    (-p.im, p.re), with c = conj(p) (correlators.h:173-176)."""
+def factor(p):
+    """(scale, q) with p = scale * q and every q component in [-128, 127] (the
+    gcd of the nonzero components), or None: config 5's +-500 QPSK pattern is
+    500 * (+-1)."""
+    a = np.abs(p.astype(np.int64)).reshape(-1)
+    a = a[a > 0]
+    g = int(np.gcd.reduce(a)) if len(a) else 1
+    q = p.astype(np.int64) // g
+    if q.min() < -128 or q.max() > 127:
+        return None
+    return g, q
+
+
+def btables(p, pl=2):
+    """The kernel's LDS B image, per kind 4 copies shifted by sigma; copy sigma
+    entry e holds the coefficient pair of tap k = e - sigma - 32 (zero outside
+    [0, 1023]); pair = (comp 0, comp 1) = re output: (c.re, -c.im) = (p.re,
+    p.im); im output: (c.im, c.re) = (-p.im, p.re), with c = conj(p)
+    (correlators.h:173-176).  pl = 2: kinds re lo, re hi, im lo, im hi of p;
+    pl = 1: kinds re, im of q = p / scale (factor()).  Returns (image, bias,
+    scale)."""
+    scale = 1
+    if pl == 1:
+        scale, p = factor(p)
     p = p.astype(np.int64)
     pairs = {"re": np.stack([p[:, 0], p[:, 1]], 1), "im": np.stack([-p[:, 1], p[:, 0]], 1)}
-    img = np.zeros(4 * BKIND, np.uint8)
+    kinds = [("re", 0), ("re", 1), ("im", 0), ("im", 1)] if pl == 2 else [("re", None), ("im", None)]
+    img = np.zeros(len(kinds) * BKIND, np.uint8)
     bias = {}
-    for ki, (out, limb) in enumerate([("re", 0), ("re", 1), ("im", 0), ("im", 1)]):
-        lo, hi = limbs(pairs[out])
-        v = (lo if limb == 0 else hi).view(np.uint8)  # (1024, 2)
+    for ki, (out, limb) in enumerate(kinds):
+        if limb is None:
+            v = pairs[out].astype(np.int8).view(np.uint8)
+        else:
+            lo, hi = limbs(pairs[out])
+            v = (lo if limb == 0 else hi).view(np.uint8)  # (1024, 2)
         bias[out] = int((128 * pairs[out].sum()) % (1 << 32))
         for sig in range(4):
             base = ki * BKIND + COPY_OFF[sig]
@@ -86,7 +108,7 @@ def btables(p):
             a = np.zeros((BENT, 2), np.uint8)
             a[ok] = v[k[ok]]
             img[base:base + 2 * BENT] = a.reshape(-1)
-    return img, bias
+    return img, bias, scale
 
 
 def coeff_scaling(p):
@@ -116,9 +138,9 @@ def oracle_registers(p, x, win=1 << 20, workers=16):
     return corr, en
 
 
-def emulate(p, x, n_out):
-    """numpy replay of corr_mfma_i8's fragments for outputs [0, n_out)."""
-    img, bias = btables(p)
+def emulate(p, x, n_out, pl=2):
+    """numpy replay of corr_mfma_i8<pl>'s fragments for outputs [0, n_out)."""
+    img, bias, scale = btables(p, pl)
     cs = coeff_scaling(p)
     L = len(x)
     xs = np.zeros((n_out + NP, 2), np.int64)  # staged samples j = -1024 .. n_out - 1
@@ -132,14 +154,15 @@ def emulate(p, x, n_out):
         acc = {k: np.zeros((32, 32), np.int64) for k in ("s0r", "s1r", "s2r", "s0i", "s1i", "s2i")}
         for t in range(CHUNKS):
             A = {}
-            for nm, pl in (("xl", xl), ("xh", xh)):
+            for nm, plane in (("xl", xl), ("xh", xh)):
                 a = np.zeros((32, 2, 16), np.int64)  # [row][h][byte]
                 for h in range(2):
                     j = iw + 32 * np.arange(32)[:, None] + 16 * t + 8 * h + np.arange(8)[None, :]  # local (+1024)
-                    a[:, h, :] = pl[j].reshape(32, 16)
+                    a[:, h, :] = plane[j].reshape(32, 16)
                 A[nm] = a
             B = {}
-            for ki, nm in enumerate(("rl", "rh", "il", "ih")):
+            names = ("rl", "rh", "il", "ih") if pl == 2 else ("rl", "il")
+            for ki, nm in enumerate(names):
                 b = np.zeros((32, 2, 16), np.int64)  # [col][h][byte]
                 for col in range(32):
                     sig = (col + 1) & 3
@@ -152,11 +175,13 @@ def emulate(p, x, n_out):
             def mm(a, b):
                 return np.einsum("rhj,chj->rc", a, b)
             acc["s0r"] += mm(A["xl"], B["rl"]); acc["s0i"] += mm(A["xl"], B["il"])
-            acc["s1r"] += mm(A["xl"], B["rh"]) + mm(A["xh"], B["rl"]); acc["s1i"] += mm(A["xl"], B["ih"]) + mm(A["xh"], B["il"])
-            acc["s2r"] += mm(A["xh"], B["rh"]); acc["s2i"] += mm(A["xh"], B["ih"])
+            acc["s1r"] += mm(A["xh"], B["rl"]); acc["s1i"] += mm(A["xh"], B["il"])
+            if pl == 2:
+                acc["s1r"] += mm(A["xl"], B["rh"]); acc["s1i"] += mm(A["xl"], B["ih"])
+                acc["s2r"] += mm(A["xh"], B["rh"]); acc["s2i"] += mm(A["xh"], B["ih"])
         m32 = (1 << 32) - 1
-        cr = (acc["s0r"] + (acc["s1r"] << 8) + (acc["s2r"] << 16) + bias["re"]) & m32
-        ci = (acc["s0i"] + (acc["s1i"] << 8) + (acc["s2i"] << 16) + bias["im"]) & m32
+        cr = (scale * (acc["s0r"] + (acc["s1r"] << 8) + (acc["s2r"] << 16) + bias["re"])) & m32
+        ci = (scale * (acc["s0i"] + (acc["s1i"] << 8) + (acc["s2i"] << 16) + bias["im"])) & m32
         tr = (cr.astype(np.uint32).view(np.int32).astype(np.int64) >> cs) >> 2
         ti = (ci.astype(np.uint32).view(np.int32).astype(np.int64) >> cs) >> 2
         c = (tr * tr + ti * ti) & m32
@@ -171,42 +196,16 @@ def run_gpu(args, p, x):
     lib.tune_corr_mfma_geometry(geo)
     assert (geo[1], geo[2], geo[3], geo[4]) == (CHUNKS, BENT, BSTRIDE, BKIND), list(geo)
     lib.tune_corr_mfma.argtypes = [C.c_void_p, C.c_long, C.c_void_p, C.c_int, C.c_uint32, C.c_uint32, C.c_void_p,
-                                   C.c_void_p, C.c_int, C.c_int, C.c_void_p]
-    img, bias = btables(p)
+                                   C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_uint32, C.c_void_p]
     cs = coeff_scaling(p)
     n = len(x)
     dx = torch.from_numpy(x).cuda()
-    db = torch.from_numpy(img).cuda()
     dc = torch.zeros(n, dtype=torch.int32, device="cuda")
     de = torch.zeros(n, dtype=torch.int32, device="cuda")
     st = torch.cuda.current_stream()
-
-    def launch(store_all, grid=args.grid):
-        rc = lib.tune_corr_mfma(C.c_void_p(dx.data_ptr()), n, C.c_void_p(db.data_ptr()), cs, bias["re"], bias["im"],
-                                C.c_void_p(dc.data_ptr()), C.c_void_p(de.data_ptr()), grid, store_all,
-                                C.c_void_p(st.cuda_stream))
-        assert rc == 0, rc
-
-    out = {"samples": n, "coeff_scaling": cs, "bias": bias, "lib": args.lib, "tile": geo[0], "lds": geo[7]}
-    if args.only_probe:  # counter passes: the probe's launches alone
-        for _ in range(args.reps):
-            launch(0)
-        torch.cuda.synchronize()
-        return
-    launch(1)
-    torch.cuda.synchronize()
-    got_c = dc.cpu().numpy().view(np.uint32)
-    got_e = de.cpu().numpy().view(np.uint32)
-    if not args.no_check:
-        t0 = time.time()
-        want_c, want_e = oracle_registers(p, x)
-        out["oracle_s"] = round(time.time() - t0, 1)
-        bc = np.nonzero(got_c != want_c)[0]
-        be = np.nonzero(got_e != want_e)[0]
-        out["corr_mismatches"] = int(len(bc))
-        out["energy_mismatches"] = int(len(be))
-        out["first_bad"] = [int(bc[0]) if len(bc) else None, int(be[0]) if len(be) else None]
-        print(json.dumps({"check": out}), flush=True)
+    variants = [int(v) for v in args.pattern_limbs.split(",")]
+    if factor(p) is None:
+        variants = [v for v in variants if v == 2]
 
     def timeit(fn, reps):
         for _ in range(args.warmup):
@@ -219,16 +218,53 @@ def run_gpu(args, p, x):
         torch.cuda.synchronize()
         return [a.elapsed_time(b) for a, b in ev]
 
-    ms = timeit(lambda: launch(0), args.reps)
-    ms_store = timeit(lambda: launch(1), args.reps)
-    t = float(np.mean(ms)) * 1e-3
-    macs = 16896.0 * n  # 66 chunks x 8 MFMAs x 32768 MACs per 1024 outputs
-    out["probe"] = {"ms": round(float(np.mean(ms)), 4), "ms_min": round(float(np.min(ms)), 4),
-                    "ms_with_stores": round(float(np.mean(ms_store)), 4),
-                    "gsamples_per_s": round(n / t / 1e9, 2),
-                    "i8_macs_per_s": macs / t, "i8_peak_frac": round(macs / t / I8_PEAK, 4),
-                    "useful_frac_of_macs": round(16384 / 16896, 4),
-                    "note": "every sample's corr and energy registers; stores suppressed in 'ms'"}
+    out = {"samples": n, "coeff_scaling": cs, "lib": args.lib, "tile": geo[0], "lds_2limb": geo[7]}
+    want = None
+    for pl in variants:
+        img, bias, scale = btables(p, pl)
+        db = torch.from_numpy(img).cuda()
+
+        def launch(store_all, grid=args.grid):
+            rc = lib.tune_corr_mfma(C.c_void_p(dx.data_ptr()), n, C.c_void_p(db.data_ptr()), cs, bias["re"],
+                                    bias["im"], C.c_void_p(dc.data_ptr()), C.c_void_p(de.data_ptr()), grid, store_all,
+                                    pl, scale, C.c_void_p(st.cuda_stream))
+            assert rc == 0, rc
+
+        if args.only_probe:  # counter passes: the probe's launches alone
+            for _ in range(args.reps):
+                launch(0)
+            torch.cuda.synchronize()
+            continue
+        v = {"pattern_limbs": pl, "scale": scale, "bias": bias}
+        dc.zero_()
+        de.zero_()
+        launch(1)
+        torch.cuda.synchronize()
+        got_c = dc.cpu().numpy().view(np.uint32)
+        got_e = de.cpu().numpy().view(np.uint32)
+        if not args.no_check:
+            t0 = time.time()
+            if want is None:
+                want = oracle_registers(p, x)
+            v["oracle_s"] = round(time.time() - t0, 1)
+            bc = np.nonzero(got_c != want[0])[0]
+            be = np.nonzero(got_e != want[1])[0]
+            v["corr_mismatches"] = int(len(bc))
+            v["energy_mismatches"] = int(len(be))
+            v["first_bad"] = [int(bc[0]) if len(bc) else None, int(be[0]) if len(be) else None]
+            print(json.dumps({"check": v}), flush=True)
+        ms = timeit(lambda: launch(0), args.reps)
+        ms_store = timeit(lambda: launch(1), args.reps)
+        t = float(np.mean(ms)) * 1e-3
+        macs = (16896.0 if pl == 2 else 8448.0) * n  # 66 chunks x 8 (4) MFMAs x 32768 MACs per 1024 outputs
+        v.update({"ms": round(float(np.mean(ms)), 4), "ms_min": round(float(np.min(ms)), 4),
+                  "ms_with_stores": round(float(np.mean(ms_store)), 4), "gsamples_per_s": round(n / t / 1e9, 2),
+                  "i8_macs_per_s": macs / t, "i8_peak_frac": round(macs / t / I8_PEAK, 4),
+                  "useful_frac_of_macs": round(16384 / 16896, 4),
+                  "bound_gsamples_per_s": round(I8_PEAK / (macs / n) / 1e9, 1)})
+        out[f"probe_{pl}limb"] = v
+    if args.only_probe:
+        return
     # the product on the same box: corr_scan_s1 through the Python mirror (stops at the detection)
     import srcdsp_amd as S
     g = S.FixedPatternCorrelator(NP, 1)
@@ -245,8 +281,11 @@ def run_gpu(args, p, x):
     out["product"] = {"ms": round(float(np.mean(pms)), 4), "detection": [bool(found), int(idx)],
                       "scanned_samples": int(scanned), "gsamples_per_s": round(scanned / tp / 1e9, 2),
                       "dot2_peak_frac": round(2048.0 * scanned / tp / DOT2_PEAK, 4)}
-    out["speedup_per_sample"] = round((n / t) / (scanned / tp), 2)
-    out["bounds_gsamples_per_s"] = {"i8_mfma_limb_formulation": round(I8_PEAK / 16896 / 1e9, 1),
+    for pl in variants:
+        v = out[f"probe_{pl}limb"]
+        v["speedup_per_sample_vs_product"] = round(v["gsamples_per_s"] / out["product"]["gsamples_per_s"], 2)
+    out["bounds_gsamples_per_s"] = {"i8_mfma_2limb": round(I8_PEAK / 16896 / 1e9, 1),
+                                    "i8_mfma_1limb": round(I8_PEAK / 8448 / 1e9, 1),
                                     "v_dot2": round(DOT2_PEAK / 2048 / 1e9, 1)}
     print(json.dumps(out), flush=True)
 
@@ -261,15 +300,21 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--only-probe", action="store_true", help="launch the probe --reps times, nothing else")
+    ap.add_argument("--pattern-limbs", default="2,1",
+                    help="variants: 2 (any pattern), 1 (pattern = gcd x int8, when it factors)")
     args = ap.parse_args()
     p, x = config5_buffer(args.samples)
     if args.emulate:
         n = args.emulate
-        got = emulate(p, x, n)
         want, _ = oracle_registers(p, x[:n])
-        bad = np.nonzero(got != want)[0]
-        print(f"emulate: {n} outputs, {len(bad)} differ from the oracle" + (f" (first {bad[0]})" if len(bad) else ""))
-        sys.exit(1 if len(bad) else 0)
+        nbad = 0
+        for pl in (2, 1):
+            got = emulate(p, x, n, pl)
+            bad = np.nonzero(got != want)[0]
+            nbad += len(bad)
+            print(f"emulate ({pl}-limb pattern): {n} outputs, {len(bad)} differ from the oracle"
+                  + (f" (first {bad[0]})" if len(bad) else ""))
+        sys.exit(1 if nbad else 0)
     run_gpu(args, p, x)
 
 
