@@ -92,6 +92,15 @@ __device__ __forceinline__ int sample_addr(int js)
     return 64 * g + 16 * (((js >> 3) & 3) ^ ((g >> 2) & 3)) + 2 * (js & 7);
 }
 
+// a B fragment: 16 bytes at an 8-B aligned LDS address, as two b64 halves (a
+// v4i load would be emitted as one ds_read_b128, which the LDS accepts at 8-B
+// alignment in unaligned mode but serves ~2.4x slower: measured, round 6)
+__device__ __forceinline__ v4i ld_b64x2(const unsigned char* p)
+{
+    const v2i a = *(const v2i*)p, b = *(const v2i*)(p + 8);
+    return v4i{a[0], a[1], b[0], b[1]};
+}
+
 __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
 {
     return __builtin_amdgcn_perm(hi, lo, sel);
@@ -223,13 +232,13 @@ corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ bta
             f.xl = *(const v4i*)(pa + ao);
             f.xh = *(const v4i*)(pa + PLANE + ao);
             const int bo = 32 * t;
-            f.rl = *(const v4i*)(pb + bo);  // 8-B aligned: two b64 halves
+            f.rl = ld_b64x2(pb + bo);
             if constexpr (PL == 2) {
-                f.rh = *(const v4i*)(pb + BKIND + bo);
-                f.il = *(const v4i*)(pb + 2 * BKIND + bo);
-                f.ih = *(const v4i*)(pb + 3 * BKIND + bo);
+                f.rh = ld_b64x2(pb + BKIND + bo);
+                f.il = ld_b64x2(pb + 2 * BKIND + bo);
+                f.ih = ld_b64x2(pb + 3 * BKIND + bo);
             } else {
-                f.il = *(const v4i*)(pb + BKIND + bo);
+                f.il = ld_b64x2(pb + BKIND + bo);
             }
             return f;
         };
