@@ -631,6 +631,29 @@ def cpu_topology():
     return cpus, sorted(first.values())
 
 
+def cpu_quota():
+    """The cgroup CPU bandwidth limit of this process, as a note: on a shared
+    GPU box the affinity mask can list every hardware thread while the
+    scheduler grants the job only a quota of CPU time (cgroup v2 cpu.max, or
+    v1 cfs_quota_us / cfs_period_us); threads beyond it share that time."""
+    for path, parse in (("/sys/fs/cgroup/cpu.max", lambda t: t.split()),
+                        ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", None)):
+        try:
+            with open(path) as f:
+                txt = f.read().strip()
+        except OSError:
+            continue
+        if parse is not None:
+            q, per = parse(txt)[:2]
+        else:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                q, per = txt, f.read().strip()
+        if q in ("max", "-1"):
+            return f"no cgroup CPU quota ({path}: {txt})"
+        return f"cgroup CPU quota {int(q) / int(per):.1f} CPUs ({path}: {txt})"
+    return "cgroup CPU quota unknown"
+
+
 def _ref_decim_lib():
     path = os.path.join(ROOT, "oracle", "_ref", "strict", "libref_decim_old.so")
     if not os.path.exists(path):
@@ -727,6 +750,7 @@ def cpu_baseline_allcores(args, threads=None):
     out = fig(cpus, f"every hardware thread of the affinity mask, machine nproc {os.cpu_count()}")
     out["physical_cores"] = fig(phys, "one per physical core")
     out["job_share"] = fig(cpus[:share], share_note)
+    out["cpu_quota"] = cpu_quota()
     return out
 
 

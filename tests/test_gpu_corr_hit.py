@@ -196,27 +196,77 @@ class CapiCorr:
 def _bind(lib):
     from srcdsp_amd._capi import SIGNATURES
     for name, (res, args) in SIGNATURES.items():
-        if name.startswith("srcdsp_corr_"):
+        if name.startswith("srcdsp_corr_") or name == "srcdsp_build_flags":
             fn = getattr(lib, name)
             fn.restype, fn.argtypes = res, args
     return lib
 
 
+# ------------------------------------- the always-exact build, in its own process
+def sweep_case(N, S_):
+    """The fuzz stream of the band sweep: QPSK pattern copies at three
+    amplitudes in noise (detections inside and outside the 1e-9 band)."""
+    from srcdsp_amd.design import qpsk_pattern
+    p = qpsk_pattern(N, 500, seed=N + 7)
+    rng = np.random.default_rng(N * 31 + S_)
+    n = 1 << 16 if N >= 1000 else 1 << 17
+    x = rng.integers(-125, 126, size=(n, 2)).astype(np.int32)
+    for off in (n // 5, n // 2, (4 * n) // 5):
+        amp = int(rng.integers(1, 4))
+        for m in range(N):
+            if off + m * S_ < n:
+                x[off + m * S_] += amp * p[m]
+    return p, np.clip(x, -32768, 32767).astype(np.int16)
+
+
+def sweep_vs_oracle(obj, oracle, p, x) -> list[str]:
+    """Step obj and the oracle through x, stepping on after every detection;
+    detections, indices, bitSamples and registers must agree."""
+    fails = []
+    for o in (obj, oracle):
+        o.set_pattern(p)
+    pos, n = 0, len(x)
+    while pos < n and not fails:
+        xs = x[pos:pos + 17000]
+        r, w = obj.step(xs), oracle.step(xs)
+        if (r[0], r[0] and r[1]) != (w[0], w[0] and w[1]):
+            fails.append(f"at {pos}: {r} vs oracle {w}")
+        elif not np.array_equal(obj.bit_samples(), oracle.bit_samples()):
+            fails.append(f"at {pos}: bitSamples")
+        else:
+            st, so = obj.status(), oracle.status()
+            if st["energy"] != list(so["energy"]) or st["corr"] != list(so["corr"]):
+                fails.append(f"at {pos}: registers {st} vs {so}")
+        pos += (w[1] + 2) if w[0] else len(xs)
+    return fails
+
+
+SWEEP = [(1024, 1), (32, 4), (64, 2), (33, 1), (127, 2), (16, 16), (1000, 1), (48, 3), (256, 4), (17, 1), (129, 1)]
+
+
 @pytest.fixture(scope="module")
-def exact_lib(S):
-    lib = _bind(C.CDLL(_need(EXACT), mode=C.RTLD_LOCAL))
-    lib.srcdsp_build_flags.restype, lib.srcdsp_build_flags.argtypes = C.c_int, [C.POINTER(C.c_uint)]
-    return lib
+def exact_results(S, tmp_path_factory):
+    """the always-exact build runs in a CHILD process that loads
+    only that library (tests/corr_exact_child.py), so its C-ABI calls and
+    kernel launches cannot resolve to the product library this process holds
+    (a kernel of each library reports its build switch: round 6 saw the
+    RTLD_LOCAL copy launch the product's kernel in-process)."""
+    import json
+    import subprocess
+    import sys
+    out = str(tmp_path_factory.mktemp("exact") / "exact.json")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "corr_exact_child.py"), _need(EXACT), out],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return json.load(open(out))
 
 
-def test_exact_build_runs_its_own_kernels(S, exact_lib):
-    """the always-exact build is loaded RTLD_LOCAL beside the
-    product library (RTLD_GLOBAL) with the same exported names; a kernel of
-    each library reports its own build switch, so the sweep below really runs
-    the always-exact kernels and not the product's."""
+def test_exact_build_runs_its_own_kernels(S, exact_results):
+    """The child holds no product library and its kernel reports the
+    always-exact switch; the product's kernel reports none."""
+    assert exact_results["product_mapped"] is False
+    assert exact_results["build_flags"] == 1  # SRCDSP_BUILD_CORR_ALWAYS_EXACT
     f = C.c_uint(99)
-    assert exact_lib.srcdsp_build_flags(C.byref(f)) == 0 and f.value == 1  # SRCDSP_BUILD_CORR_ALWAYS_EXACT
-    f.value = 99
     assert S.lib().srcdsp_build_flags(C.byref(f)) == 0 and f.value == 0
 
 
@@ -231,42 +281,20 @@ def test_tie_streams_through_the_product(S, case, host):
 
 
 @pytest.mark.parametrize("case", MAN["cases"], ids=lambda c: c["key"])
-def test_tie_streams_through_the_always_exact_build(exact_lib, case):
-    assert T.replay(case, ARR, CapiCorr(exact_lib, case["N"], case["S"])) == []
+def test_tie_streams_through_the_always_exact_build(exact_results, case):
+    assert exact_results["ties"][case["key"]] == []
 
 
-@pytest.mark.parametrize("N,S_", [(1024, 1), (32, 4), (64, 2), (33, 1), (127, 2), (16, 16), (1000, 1),
-                                  (48, 3), (256, 4), (17, 1), (129, 1)])
-def test_band_sweep_always_exact_equals_product(S, O, exact_lib, N, S_):
+@pytest.mark.parametrize("N,S_", SWEEP)
+def test_band_sweep_product_and_always_exact_vs_oracle(S, O, exact_results, N, S_):
     """Threshold sweep: the build whose band is infinite (every peak decided
-    by the correctly rounded square roots) gives the product's detections,
-    indices, bitSamples and registers on the fuzz streams of
-    test_correlator_vs_oracle, stepping on after every detection; the oracle
-    agrees with both."""
-    from srcdsp_amd.design import qpsk_pattern
-    p = qpsk_pattern(N, 500, seed=N + 7)
-    rng = np.random.default_rng(N * 31 + S_)
-    n = 1 << 16 if N >= 1000 else 1 << 17
-    x = rng.integers(-125, 126, size=(n, 2)).astype(np.int32)
-    for off in (n // 5, n // 2, (4 * n) // 5):
-        amp = int(rng.integers(1, 4))
-        for m in range(N):
-            if off + m * S_ < n:
-                x[off + m * S_] += amp * p[m]
-    x = np.clip(x, -32768, 32767).astype(np.int16)
-    objs = [CapiCorr(S.lib(), N, S_), CapiCorr(exact_lib, N, S_), O["fma"].corr(N, S_)]
-    for o in objs:
-        o.set_pattern(p)
-    pos = 0
-    while pos < n:
-        xs = x[pos:pos + 17000]
-        res = [o.step(xs) for o in objs]
-        assert res[0] == res[1] and (res[0][0], res[0][0] and res[0][1]) == (res[2][0], res[2][0] and res[2][1])
-        for o in objs[:2]:
-            assert np.array_equal(o.bit_samples(), objs[2].bit_samples())
-            st, so = o.status(), objs[2].status()
-            assert st["energy"] == list(so["energy"]) and st["corr"] == list(so["corr"])
-        pos += (res[2][1] + 2) if res[2][0] else len(xs)
+    by the correctly rounded square roots, in the child process) and the
+    product each give the oracle's detections, indices, bitSamples and
+    registers on the fuzz streams, stepping on after every detection; so the
+    product's fast sign test equals the exact one there."""
+    p, x = sweep_case(N, S_)
+    assert sweep_vs_oracle(CapiCorr(S.lib(), N, S_), O["fma"].corr(N, S_), p, x) == []
+    assert exact_results["sweep"][f"{N}_{S_}"] == []
 
 
 def _oracle_trace(o, x):
