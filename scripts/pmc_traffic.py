@@ -68,8 +68,11 @@ def main():
         a.samples = (1 << 26) if a.workload == "corr" else (1 << 28)
     key = KERNEL_KEYS[a.workload]
     steps_run = 6  # bench.py --warmup 1 --steps 5: every step's dispatches are counted
+    # --no-parity: the decim line's post-timing parity step is one more launch of
+    # the same kernel; counters are summed over dispatches and divided by the
+    # steps run, so it must not run here (round 6: it read as 7/6 x the traffic)
     bench_args = ["--workload", a.workload, "--steps", "5", "--warmup", "1", "--no-cpu-baseline", "--no-pcie",
-                  "--samples", str(a.samples)]
+                  "--no-parity", "--samples", str(a.samples)]
     if a.channels > 1:
         bench_args += ["--channels-per-gpu", str(a.channels)]
     res = {}

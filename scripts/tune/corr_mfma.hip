@@ -57,6 +57,9 @@ typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 namespace {
 constexpr int NP = 1024;                 // pattern length (config 5)
+#ifndef WG_DESYNC
+#define WG_DESYNC 0                      // s_sleep(127) rounds (~8k cycles each) for the second workgroup per CU
+#endif
 #ifndef CORR_WAVES
 #define CORR_WAVES 8                     // waves per workgroup (8: one workgroup per CU)
 #endif
@@ -163,6 +166,15 @@ corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ bta
         }
     };
     if (blockIdx.x < n_tiles) fetch(blockIdx.x);
+#if WG_DESYNC
+    // two workgroups per CU start in phase and, doing identical work, stay in
+    // phase: their staging / scan / epilogue phases coincide and the MFMAs
+    // idle.  The second half of the grid (the second workgroup a CU receives)
+    // starts about half a tile later, so one's non-MFMA phases run under the
+    // other's MFMAs (tuning experiment).
+    if (WG_PER_CU > 1 && blockIdx.x >= gridDim.x / 2)
+        for (int i = 0; i < WG_DESYNC; ++i) __builtin_amdgcn_s_sleep(127);
+#endif
 
     for (long tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
         const long i0 = tile * TILE;
