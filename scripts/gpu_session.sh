@@ -26,6 +26,8 @@
 #                    (scripts/tune/ab_libs.sh; WORKLOADS, ROUNDS, LAUNCHES)
 #   dist             the 2-rank GPU test of the N > 1 path (tests/test_gpu_dist.py)
 #   cpp              the drop-in C++ tests (tests/test_dropin_cpp.py -m gpu)
+#   merge            scripts/merge_pmc.py ${TAG} on the box, so a later bench step in the same session reports the
+#                    traffic just measured (merge locally too: gpurun_out/ comes back, profiles/ does not)
 #   mfma             the integer matrix-core probes (tuning only, never shipped): config 5's correlator
 #                    (scripts/tune/corr_mfma.py ${CORR_ARGS}, for each of ${CORR_LIBS}) and config 4's tap loop
 #                    (scripts/tune/mixdecim_mfma.py ${MIX_ARGS}), each checked against the oracle and timed
@@ -94,6 +96,8 @@ for s in ${STEPS:-smoke tests bench}; do
     census) step census_$TAG 120 python -u scripts/tune/census.py ;;
     ab) step ab_$TAG 1000 bash scripts/tune/ab_libs.sh ;;
     dist) step dist_$TAG 300 python -u -m pytest tests/test_gpu_dist.py -m gpu -v --timeout 240 --timeout-method thread ;;
+    merge)  # this session's PMC entries into profiles/pmc_traffic.json (on the box: a later bench step reports them)
+      step merge_$TAG 60 python -u scripts/merge_pmc.py $TAG ;;
     mfma)
       for lib in ${CORR_LIBS:-libcorrmfma.so}; do
         step corrmfma_${lib%.so}_$TAG 400 python -u scripts/tune/corr_mfma.py --lib $lib ${CORR_ARGS}
