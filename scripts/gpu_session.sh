@@ -50,7 +50,7 @@ for s in ${STEPS:-smoke tests bench}; do
   case $s in
     smoke) step smoke_$TAG 300 python -u __graft_entry__.py smoke ;;
     tests) step tests_$TAG 1000 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread \
-             --maxfail=30 ${PYTEST_K:+-k "$PYTEST_K"} ;;
+             --maxfail=30 --durations=25 ${PYTEST_K:+-k "$PYTEST_K"} ;;
     bench) step bench_$TAG 300 python -u bench.py ${BENCH_ARGS:---steps 20 --warmup 5} ;;
     bench_all)
       for w in decim mixdecim ci16decim corr fir up; do

@@ -88,7 +88,8 @@ def test_bench_two_rank_rehearsal_default_layout():
     RCCL communicator): the main series is one 2^28 channel per rank (the
     N = 1 line's work per GPU, weak scaling); `configs2_share` beside it runs
     8 channels per rank, labelled as configs[2]'s per-GPU layout (16 of 64),
-    and its timed gather moves all 16 channels' outputs (8 GiB) to rank 0."""
+    and its timed gather moves all 16 channels' outputs (8 GiB) to rank 0;
+    both report 0 mismatches against the channel digests."""
     import json
     import torch
     if torch.cuda.device_count() < 1:
@@ -114,3 +115,9 @@ def test_bench_two_rank_rehearsal_default_layout():
     assert sh["gather_bytes"] == 16 * (1 << 26) * 8 and sh["gather_ms"] > 0
     assert sh["roofline"]["channels_per_launch"] == 8
     assert sh["roofline"]["algorithmic_bytes_per_launch"] == 8 * (1 << 28) * 10
+    # cross-rank parity: every rank's channels and what the gather
+    # delivered equal the oracle/reference digests (tests/golden/channel_digests.json)
+    p = line["parity"]
+    assert (p["channels_checked"], p["mismatches"], p["missing"]) == (2, 0, 0), p
+    assert (sh["parity"]["channels_checked"], sh["parity"]["mismatches"]) == (16, 0), sh["parity"]
+    assert (sh["gather_parity"]["channels_checked"], sh["gather_parity"]["mismatches"]) == (16, 0)
