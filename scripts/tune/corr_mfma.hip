@@ -60,6 +60,12 @@ constexpr int NP = 1024;                 // pattern length (config 5)
 #ifndef WG_DESYNC
 #define WG_DESYNC 0                      // s_sleep(127) rounds (~8k cycles each) for the second workgroup per CU
 #endif
+#ifndef PROBE_SKIP_A
+#define PROBE_SKIP_A 0
+#endif
+#ifndef PROBE_SKIP_B
+#define PROBE_SKIP_B 0
+#endif
 #ifndef CORR_WAVES
 #define CORR_WAVES 8                     // waves per workgroup (8: one workgroup per CU)
 #endif
@@ -257,7 +263,17 @@ corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ bta
         Frags cur = load(0);
 #pragma unroll 2
         for (int t = 0; t < CHUNKS; ++t) {
+#if PROBE_SKIP_A || PROBE_SKIP_B
+            // LDS-bound test (wrong results): odd chunks reuse the previous
+            // chunk's A (or B) fragments instead of reading them
+            Frags nxt = load(t + 1 < CHUNKS ? t + 1 : t);
+            if ((t + 1) & 1) {
+                if (PROBE_SKIP_A) { nxt.xl = cur.xl; nxt.xh = cur.xh; }
+                if (PROBE_SKIP_B) { nxt.rl = cur.rl; nxt.rh = cur.rh; nxt.il = cur.il; nxt.ih = cur.ih; }
+            }
+#else
             const Frags nxt = load(t + 1 < CHUNKS ? t + 1 : t);
+#endif
             s0r = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl, cur.rl, s0r, 0, 0, 0);
             s0i = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl, cur.il, s0i, 0, 0, 0);
             if constexpr (PL == 2) {
