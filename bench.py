@@ -825,6 +825,17 @@ def cpu_baseline_other(args, pyoracle):
                       f"host CPU: {_cpu_model()}"}
 
 
+def host_leg(fn, *a, **kw):
+    """A host-side leg of the line (CPU baselines): its failure on an unusual
+    host (no reference build, a CPU the affinity call refuses) is reported in
+    the line instead of losing the line after the GPU measurement."""
+    try:
+        return fn(*a, **kw)
+    except Exception as e:  # noqa: BLE001
+        print(f"bench: {fn.__name__} failed: {e!r}", file=sys.stderr, flush=True)
+        return {"error": f"{type(e).__name__}: {e}"}
+
+
 def pcie_inclusive(S):
     """The reference-style host std::vector step() (srcdsp_decim_step_host):
     host input staged through pinned memory, H2D, the same kernel, D2H.  A side
@@ -1180,11 +1191,11 @@ def main(argv=None, S=None, dev=None):
         if args.workload == "corr":
             line["detection"] = list(work.last)
         if not args.no_cpu_baseline and world == 1:
-            line["cpu_baseline"] = cpu_baseline(args)
+            line["cpu_baseline"] = host_leg(cpu_baseline, args)
             if args.workload == "decim":
-                line["cpu_baseline_allcores"] = cpu_baseline_allcores(args)
+                line["cpu_baseline_allcores"] = host_leg(cpu_baseline_allcores, args)
                 # the reference-equivalent -O0 build, for context
-                line["cpu_baseline_O0"] = cpu_baseline(args, "O0", sample=1 << 24)
+                line["cpu_baseline_O0"] = host_leg(cpu_baseline, args, "O0", sample=1 << 24)
         if args.workload == "decim" and world == 1 and not args.no_pcie:
             line["pcie_inclusive"] = pcie_inclusive(S)
         print(json.dumps(line), flush=True)

@@ -185,3 +185,28 @@ def test_bench_main_one_rank_with_share_on_host():
     assert line["parity"]["channels_checked"] == 1 and line["parity"]["mismatches"] == 0
     sh = line["configs2_share"]
     assert sh["parity"]["channels_checked"] == 8 and "gather_ms" not in sh
+
+
+def test_host_leg_reports_a_failure_instead_of_raising():
+    def boom(args):
+        raise OSError("affinity refused")
+    assert bench.host_leg(boom, None) == {"error": "OSError: affinity refused"}
+    assert bench.host_leg(lambda a, b=1: a + b, 1, b=2) == 3
+
+
+def test_cpu_topology_and_quota():
+    cpus, phys = bench.cpu_topology()
+    assert cpus and phys and set(phys) <= set(cpus) and len(phys) <= len(cpus)
+    assert "cgroup CPU quota" in bench.cpu_quota() or "no cgroup CPU quota" in bench.cpu_quota()
+
+
+@pytest.mark.skipif(not os.path.exists(REF), reason="reference build (oracle/_ref) not present")
+def test_cpu_baseline_allcores_all_threads_physical_and_share():
+    """The default all-cores leg: every CPU of the affinity mask (pinned), one
+    per physical core, the job's share, and the cgroup quota note."""
+    a = types.SimpleNamespace(workload="decim", cpu_sample=1 << 18, samples=1 << 16)
+    r = bench.cpu_baseline_allcores(a)
+    cpus, phys = bench.cpu_topology()
+    assert r["cores"] == len(cpus) and r["value"] > 0 and "every hardware thread" in r["sample"]
+    assert r["physical_cores"]["cores"] == len(phys) and r["physical_cores"]["value"] > 0
+    assert r["job_share"]["cores"] == min(len(cpus), bench.host_cores()[0]) and "cpu_quota" in r
