@@ -66,6 +66,9 @@ constexpr int NP = 1024;                 // pattern length (config 5)
 #ifndef PROBE_SKIP_B
 #define PROBE_SKIP_B 0
 #endif
+#ifndef CORR_PREFETCH
+#define CORR_PREFETCH 1                  // 0: no register prefetch of the next tile / next chunk (fewer VGPRs)
+#endif
 #ifndef CORR_WAVES
 #define CORR_WAVES 8                     // waves per workgroup (8: one workgroup per CU)
 #endif
@@ -87,7 +90,7 @@ template <int PL> constexpr int BBYTES = 2 * PL * BKIND;
 constexpr int LDS_A = 2 * PLANE;
 constexpr int LDS_P = SPAN * 4;
 template <int PL> constexpr int LDS_TOTAL = BBYTES<PL> + LDS_A + LDS_P + WAVES * 4;
-constexpr int WG_PER_CU = 8 / WAVES;     // 2 waves per SIMD either way
+constexpr int WG_PER_CU = WAVES >= 8 ? 1 : 8 / WAVES;  // 4, 8: 2 waves per SIMD; 12: 3
 static_assert(2360 >= BSTRIDE && 4728 - 2360 >= BSTRIDE && 7096 - 4728 >= BSTRIDE, "B copies overlap");
 static_assert(SPAN % 32 == 0 && TILE % 1024 == 0, "tile shape");
 static_assert(WG_PER_CU * LDS_TOTAL<2> <= 160 * 1024, "LDS");
@@ -171,7 +174,7 @@ corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ bta
                 pre[k] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 0));
         }
     };
-    if (blockIdx.x < n_tiles) fetch(blockIdx.x);
+    if (CORR_PREFETCH && blockIdx.x < n_tiles) fetch(blockIdx.x);
 #if WG_DESYNC
     // two workgroups per CU start in phase and, doing identical work, stay in
     // phase: their staging / scan / epilogue phases coincide and the MFMAs
@@ -184,6 +187,7 @@ corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ bta
 
     for (long tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
         const long i0 = tile * TILE;
+        if (!CORR_PREFETCH) fetch(tile);
         __syncthreads();          // previous tile's readers are done with A and P
         // ---- staging: the prefetched granules -> limb planes and |x|^2
 #pragma unroll
@@ -208,16 +212,15 @@ corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ bta
             *(v4u*)(ldsP + js) = p;
         }
         __syncthreads();
-        if (tile + gridDim.x < n_tiles) fetch(tile + gridDim.x);
+        if (CORR_PREFETCH && tile + gridDim.x < n_tiles) fetch(tile + gridDim.x);
         // ---- energy: inclusive prefix of |x|^2 over the span (18 samples per lane)
         {
-            constexpr int PER = SPAN / LANES;  // 18
-            static_assert(SPAN % LANES == 0, "scan split");
+            constexpr int PER = (SPAN + LANES - 1) / LANES;  // 18 (a ragged last lane when LANES does not divide SPAN)
             uint32_t loc[PER];
             uint32_t s = 0;
 #pragma unroll
             for (int q = 0; q < PER; ++q) {
-                s += ldsP[PER * tid + q];
+                if (SPAN % LANES == 0 || PER * tid + q < SPAN) s += ldsP[PER * tid + q];
                 loc[q] = s;
             }
             // wave-inclusive scan of the lane totals
@@ -233,7 +236,7 @@ corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ bta
             for (int q = 0; q < w; ++q) base += ldsW[q];
 #pragma unroll
             for (int q = 0; q < PER; ++q)
-                ldsP[PER * tid + q] = loc[q] + base;
+                if (SPAN % LANES == 0 || PER * tid + q < SPAN) ldsP[PER * tid + q] = loc[q] + base;
         }
         __syncthreads();
 
@@ -271,8 +274,10 @@ corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ bta
                 if (PROBE_SKIP_A) { nxt.xl = cur.xl; nxt.xh = cur.xh; }
                 if (PROBE_SKIP_B) { nxt.rl = cur.rl; nxt.rh = cur.rh; nxt.il = cur.il; nxt.ih = cur.ih; }
             }
-#else
+#elif CORR_PREFETCH
             const Frags nxt = load(t + 1 < CHUNKS ? t + 1 : t);
+#else
+            cur = load(t);
 #endif
             s0r = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl, cur.rl, s0r, 0, 0, 0);
             s0i = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl, cur.il, s0i, 0, 0, 0);
@@ -284,7 +289,9 @@ corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ bta
             }
             s1r = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh, cur.rl, s1r, 0, 0, 0);
             s1i = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh, cur.il, s1i, 0, 0, 0);
+#if CORR_PREFETCH || PROBE_SKIP_A || PROBE_SKIP_B
             cur = nxt;
+#endif
         }
 
         // ---- epilogue: D layout col = l & 15.. 31, row = (r & 3) + 8 (r >> 2) + 4 h
