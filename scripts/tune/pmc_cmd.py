@@ -36,7 +36,25 @@ def one(cmd, ksub, counters, tag):
         per.setdefault(d, {}).setdefault(row["Counter_Name"], 0.0)
         per[d][row["Counter_Name"]] += float(row["Counter_Value"])
     ds = sorted(per, key=lambda k: int(k))[2:]
-    return {c: sum(per[d].get(c, 0.0) for d in ds) / max(1, len(ds)) for c in counters} | {"dispatches": len(ds)}
+    res = {c: sum(per[d].get(c, 0.0) for d in ds) / max(1, len(ds)) for c in counters} | {"dispatches": len(ds)}
+    # the same dispatches' durations from the kernel trace of this pass: the
+    # clock the kernel held (GRBM_GUI_ACTIVE sums the 8 XCDs) and, with
+    # SQ_VALU_MFMA_BUSY_CYCLES (summed over the 1024 SIMDs), the MFMA busy share
+    tr = glob.glob(os.path.join(out, "**", "*kernel_trace.csv"), recursive=True)
+    if tr:
+        dur = {}
+        for row in csv.DictReader(open(tr[0])):
+            d = row.get("Dispatch_Id") or row.get("Correlation_Id")
+            if d in per:
+                dur[d] = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9
+        if all(d in dur for d in ds) and ds:
+            t = sum(dur[d] for d in ds) / len(ds)
+            res["mean_s"] = t
+            if "GRBM_GUI_ACTIVE" in res:
+                res["clock_ghz"] = res["GRBM_GUI_ACTIVE"] / 8 / t / 1e9
+                if "SQ_VALU_MFMA_BUSY_CYCLES" in res:
+                    res["mfma_busy_frac"] = res["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / (res["GRBM_GUI_ACTIVE"] / 8)
+    return res
 
 
 def main():
@@ -44,7 +62,10 @@ def main():
     outp, ksub = sys.argv[1], sys.argv[2]
     cmd = sys.argv[sep + 1:]
     r = {}
-    for i, p in enumerate([MFMA_PASS] + PASSES):
+    passes = [MFMA_PASS] + PASSES
+    if os.environ.get("PMC_PASSES"):  # e.g. "0": the MFMA pass only
+        passes = [passes[int(i)] for i in os.environ["PMC_PASSES"].split(",")]
+    for i, p in enumerate(passes):
         res = one(cmd, ksub, p, f"p{i}")
         r[f"pass{i}"] = res
         print(i, json.dumps(res), flush=True)
