@@ -184,6 +184,28 @@ def run_gpu(args, x, c):
         torch.cuda.synchronize()
         return [a.elapsed_time(b) for a, b in ev]
 
+    if args.cold:
+        # the driver's protocol for each: an idle pause, then 5 untimed and 20
+        # timed launches (per-launch HIP events); interleaved, IDLE s apart
+        import time as _t
+        cold = {}
+        for rnd in range(args.rounds):
+            for nm, fn in (("probe", launch), ("product", prod)):
+                torch.cuda.synchronize()
+                _t.sleep(args.idle)
+                for _ in range(5):
+                    fn()
+                ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
+                for a, b in ev:
+                    a.record(st)
+                    fn()
+                    b.record(st)
+                torch.cuda.synchronize()
+                cold.setdefault(nm, []).append(round(float(np.mean([a.elapsed_time(b) for a, b in ev])), 4))
+        out["driver_protocol_ms"] = cold
+        out["driver_protocol_speedup"] = round(float(np.mean(cold["product"]) / np.mean(cold["probe"])), 3)
+        print(json.dumps(out), flush=True)
+        return
     res = {}
     for rnd in range(args.rounds):  # interleaved rounds, same box
         for nm, fn in (("probe", launch), ("product", prod)):
@@ -209,6 +231,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--only-probe", action="store_true", help="launch the probe --reps times, nothing else")
+    ap.add_argument("--cold", action="store_true",
+                    help="the driver's protocol: after --idle s, 5 untimed + 20 timed launches, probe and product")
+    ap.add_argument("--idle", type=float, default=8.0)
     args = ap.parse_args()
     c = q14(hamming_sinc(127))
     if args.emulate:
