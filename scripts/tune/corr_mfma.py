@@ -221,6 +221,8 @@ def run_gpu(args, p, x):
     out = {"samples": n, "coeff_scaling": cs, "lib": args.lib, "tile": geo[0], "lds_2limb": geo[7]}
     want = None
     for pl in variants:
+        if args.cold:
+            break
         img, bias, scale = btables(p, pl)
         db = torch.from_numpy(img).cuda()
 
@@ -265,6 +267,41 @@ def run_gpu(args, p, x):
         out[f"probe_{pl}limb"] = v
     if args.only_probe:
         return
+    if args.cold:
+        # the driver's protocol: an idle pause, 5 untimed + 20 timed launches
+        # (per-launch HIP events), probe (each variant) and product interleaved
+        import srcdsp_amd as S
+        g = S.FixedPatternCorrelator(NP, 1)
+        g.setPattern(p)
+
+        def prod_step():
+            g.reset()
+            g.step(dx)
+        fns = {"product": prod_step}
+        for pl in variants:
+            img, bias, scale = btables(p, pl)
+            dbv = torch.from_numpy(img).cuda()
+            fns[f"probe_{pl}limb"] = (lambda dbv=dbv, bias=bias, scale=scale, pl=pl: lib.tune_corr_mfma(
+                C.c_void_p(dx.data_ptr()), n, C.c_void_p(dbv.data_ptr()), cs, bias["re"], bias["im"],
+                C.c_void_p(dc.data_ptr()), C.c_void_p(de.data_ptr()), args.grid, 0, pl, scale,
+                C.c_void_p(st.cuda_stream)))
+        cold = {}
+        for rnd in range(3):
+            for nm, fn in fns.items():
+                torch.cuda.synchronize()
+                time.sleep(args.idle)
+                for _ in range(5):
+                    fn()
+                ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
+                for a, b in ev:
+                    a.record(st)
+                    fn()
+                    b.record(st)
+                torch.cuda.synchronize()
+                cold.setdefault(nm, []).append(round(float(np.mean([a.elapsed_time(b) for a, b in ev])), 4))
+        out["driver_protocol_ms"] = cold
+        print(json.dumps(out), flush=True)
+        return
     # the product on the same box: corr_scan_s1 through the Python mirror (stops at the detection)
     import srcdsp_amd as S
     g = S.FixedPatternCorrelator(NP, 1)
@@ -300,6 +337,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--only-probe", action="store_true", help="launch the probe --reps times, nothing else")
+    ap.add_argument("--cold", action="store_true",
+                    help="the driver's protocol (after --idle s: 5 untimed + 20 timed launches), probe and product")
+    ap.add_argument("--idle", type=float, default=8.0)
     ap.add_argument("--pattern-limbs", default="2,1",
                     help="variants: 2 (any pattern), 1 (pattern = gcd x int8, when it factors)")
     args = ap.parse_args()
