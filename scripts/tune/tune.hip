@@ -244,8 +244,9 @@ extern "C" int tune_fir(int variant, int grid, const float *d_coef, const void *
     switch (variant) {
     case 0: return launch(fir_stream_f32<KV_F32_REAL, true, 1>, grid, kFirBlock, L, s);
     case 1: return launch(fir_stream_f32<KV_F32_REAL, true, 2>, grid, kFirBlock, L, s);
-    case 2: return launch(fir_stream_f32<KV_CF32, true, 1>, grid, kFirBlock, L, s);
-    case 3: return launch(fir_stream_f32<KV_CF32, true, 2>, grid, kFirBlock, L, s);
+    // variants 2, 3 (complex<float> input) are gone: fir_stream_f32 is the
+    // float -> complex<float> kernel only (FirTraits<KV_F32_REAL>); complex<float>
+    // FIRs run on the decimator kernels at M = 1
     }
     return -1;
 }
