@@ -167,7 +167,7 @@ def fir_ab(rounds=4, reps=30):
     h0 = torch.zeros(64, dtype=torch.complex64, device="cuda")
     h1 = torch.zeros(64, dtype=torch.complex64, device="cuda")
     cases = []
-    for kin, var0 in (("float", 0), ("complex<float>", 2)):
+    for kin, var0 in (("float", 0),):  # the complex<float> variants left fir_stream_f32 (tune.hip)
         if kin == "float":
             x = torch.randint(-2048, 2048, (L,), device="cuda").float()
         else:
