@@ -684,6 +684,29 @@ def test_config4_whole_output(S, O):
     torch.cuda.empty_cache()
 
 
+def test_ci16decim_bench_whole_output(S, O):
+    """Row a2 as the ci16decim bench workload runs it: FilterDnsamplingFir<ci16,
+    ci16,ci32,int32_t,4>, 127 Q14 taps, 2^28 complex<int16_t> samples of the
+    synthetic generator, one step(): EVERY one of the 2^26 outputs against the
+    oracle (dnsampling_filters.h:150-167 with dsp_complex.cpp:23-29 products)."""
+    import torch
+    import fullsize as F
+    from srcdsp_amd.design import hamming_sinc, q14
+    cq = q14(hamming_sinc(127))
+    L = 1 << 28
+    x = torch.empty((L, 2), dtype=torch.int16, device="cuda")
+    S.fill_synthetic(x, "ci16", seed=0x5EED, channel=0, lo=-8192, hi=8191)
+    d = S.FilterDnsamplingFir(cq, 4, "complex<int16_t>", "complex<int16_t>", "complex<int32_t>", "int32_t")
+    y = d.step(x).cpu().numpy()
+    xh = x.cpu().numpy()
+    want = F.decim_all(lambda: O["strict"].decim(1, 4, cq), xh, 4, 128, np.empty((L // 4, 2), np.int16))
+    bad = F.first_bad(y, want)
+    assert bad is None, f"first differing output {bad}"
+    assert d.state()["history"].tobytes() == xh[L - 126:].tobytes()
+    del x
+    torch.cuda.empty_cache()
+
+
 def test_decim_cf32_beyond_4gib_one_channel(S, O):
     """One channel past 4 GiB: 2^30 + a ragged tail of complex<float> samples
     (8 GiB in, one step()), so byte offsets pass 2^32 and sample indices 2^29:
@@ -770,12 +793,12 @@ def test_fir_and_up_bench_whole_output(S, O):
     L = 1 << 28
     x = torch.randint(-2048, 2048, (L,), device="cuda").float()
     c = hamming_sinc(31, 0.2)
-    y = S.FilterFir(c, "float", "complex<float>", "float", "float", fp="fma").step(x)
-    torch.cuda.synchronize()
     xh = x.cpu().numpy()
-    want = F.decim_all(lambda: O["fma"].fir(1, c), xh, 1, 32, np.empty(L, np.complex64))
-    bad = F.first_bad(y.cpu().numpy(), want)
-    assert bad is None, f"fir: first differing output {bad}"
+    for fp in ("fma", "strict"):  # both float contracts (filters.h:153-164 in ascending k)
+        y = S.FilterFir(c, "float", "complex<float>", "float", "float", fp=fp).step(x).cpu().numpy()
+        want = F.decim_all(lambda: O[fp].fir(1, c), xh, 1, 32, np.empty(L, np.complex64))
+        bad = F.first_bad(y, want)
+        assert bad is None, f"fir ({fp}): first differing output {bad}"
     del x, y, xh, want
     n = 1 << 26
     xu = torch.empty((n, 2), dtype=torch.int16, device="cuda")
