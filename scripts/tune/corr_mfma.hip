@@ -66,6 +66,9 @@ constexpr int NP = 1024;                 // pattern length (config 5)
 #ifndef PROBE_SKIP_B
 #define PROBE_SKIP_B 0
 #endif
+#ifndef CORR_SCHED_BARRIER
+#define CORR_SCHED_BARRIER 0             // 1: sched_barrier around the MFMAs (the prefetch stays a prefetch)
+#endif
 #ifndef CORR_PREFETCH
 #define CORR_PREFETCH 1                  // 0: no register prefetch of the next tile / next chunk (fewer VGPRs)
 #endif
@@ -276,6 +279,12 @@ corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ bta
             }
 #elif CORR_PREFETCH
             const Frags nxt = load(t + 1 < CHUNKS ? t + 1 : t);
+#if CORR_SCHED_BARRIER
+            // keep the next chunk's LDS reads above this chunk's MFMAs (the
+            // scheduler otherwise sinks them next to their use, exposing the
+            // LDS latency before an MFMA: measured, round 6)
+            __builtin_amdgcn_sched_barrier(0);
+#endif
 #else
             cur = load(t);
 #endif
@@ -290,6 +299,9 @@ corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ bta
             s1r = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh, cur.rl, s1r, 0, 0, 0);
             s1i = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh, cur.il, s1i, 0, 0, 0);
 #if CORR_PREFETCH || PROBE_SKIP_A || PROBE_SKIP_B
+#if CORR_SCHED_BARRIER
+            __builtin_amdgcn_sched_barrier(0);
+#endif
             cur = nxt;
 #endif
         }
@@ -300,6 +312,15 @@ corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ bta
         const bool full = iw + 1024 <= n;
         uint32_t* co = corr_out + iw;
         uint32_t* eo = e_out + iw;
+        // the window energies first: 32 LDS words read back to back (one wait),
+        // not one wait per output between the conditional stores below
+        uint32_t ew[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int li = 1024 * w + 32 * row + rc + NP;  // local index of output iw + 32 row + rc
+            ew[r] = ldsP[li] - ldsP[li - NP];
+        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -320,9 +341,8 @@ corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ bta
             const int32_t tr = (((int32_t)cr >> sh) << 8) >> 8;
             const int32_t ti = (((int32_t)ci >> sh) << 8) >> 8;
             const uint32_t corr = (uint32_t)(tr * tr) + (uint32_t)(ti * ti);
-            // local sample index of output iw + o is 1024 w + o + NP; window (li - 1024, li]
-            const int li = 1024 * w + o + NP;
-            const uint32_t e = (ldsP[li] - ldsP[li - NP]) >> es;
+            // window (li - 1024, li] of local sample li = 1024 w + o + NP
+            const uint32_t e = ew[r] >> es;
             if (store_all) {
                 if (full || iw + o < n) {
                     co[o] = corr;
