@@ -60,6 +60,12 @@ constexpr int NP = 1024;                 // pattern length (config 5)
 #ifndef WG_DESYNC
 #define WG_DESYNC 0                      // s_sleep(127) rounds (~8k cycles each) for the second workgroup per CU
 #endif
+#ifndef PROBE_SKIP_SCAN
+#define PROBE_SKIP_SCAN 0                // timing tests (wrong results): no energy prefix scan
+#endif
+#ifndef PROBE_SKIP_STAGE
+#define PROBE_SKIP_STAGE 0               // ... or no staging after the first tile
+#endif
 #ifndef PROBE_SKIP_A
 #define PROBE_SKIP_A 0
 #endif
@@ -194,7 +200,7 @@ corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ bta
         __syncthreads();          // previous tile's readers are done with A and P
         // ---- staging: the prefetched granules -> limb planes and |x|^2
 #pragma unroll
-        for (int k = 0; k < NG; ++k) {
+        for (int k = 0; k < (PROBE_SKIP_STAGE && tile != blockIdx.x ? 0 : NG); ++k) {
             const int g = tid + LANES * k;
             if (g >= SPAN / 4) break;
             const v4u v = pre[k];
@@ -217,7 +223,7 @@ corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ bta
         __syncthreads();
         if (CORR_PREFETCH && tile + gridDim.x < n_tiles) fetch(tile + gridDim.x);
         // ---- energy: inclusive prefix of |x|^2 over the span (18 samples per lane)
-        {
+        if (!PROBE_SKIP_SCAN) {
             constexpr int PER = (SPAN + LANES - 1) / LANES;  // 18 (a ragged last lane when LANES does not divide SPAN)
             uint32_t loc[PER];
             uint32_t s = 0;
