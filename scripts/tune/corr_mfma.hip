@@ -73,7 +73,7 @@ constexpr int NP = 1024;                 // pattern length (config 5)
 #define PROBE_SKIP_B 0
 #endif
 #ifndef CORR_SCHED_BARRIER
-#define CORR_SCHED_BARRIER 0             // 1: sched_barrier around the MFMAs (the prefetch stays a prefetch)
+#define CORR_SCHED_BARRIER 1             // sched_barrier around the MFMAs (the prefetch stays a prefetch); 0: without
 #endif
 #ifndef CORR_PREFETCH
 #define CORR_PREFETCH 1                  // 0: no register prefetch of the next tile / next chunk (fewer VGPRs)
