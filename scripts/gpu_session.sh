@@ -32,6 +32,8 @@
 #                    (scripts/tune/corr_mfma.py ${CORR_ARGS}, for each of ${CORR_LIBS}) and config 4's tap loop
 #                    (scripts/tune/mixdecim_mfma.py ${MIX_ARGS}), each checked against the oracle and timed
 #                    beside the product on the same box
+#   corrlib          the correlator's fused scan on the i8 matrix cores behind the product's C ABI (tuning
+#                    library scripts/tune/ab/libsrcdsp_hip_corrmfma.so, never shipped): parity, tests, bench
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -110,6 +112,26 @@ for s in ${STEPS:-smoke tests bench}; do
       done
       step mixmfmapmc_$TAG 600 python -u scripts/tune/pmc_cmd.py gpurun_out/mixmfma_pmc_$TAG.json mixdecim_mfma_i8 \
         -- python3 scripts/tune/mixdecim_mfma.py --only-probe --reps 8 ;;
+    corrlib)  # the corrmfma tuning library behind the product's C ABI: its own seam / history / limb
+              # cases, the correlator GPU tests, then config 5's bench line beside the product's
+      L=$PWD/scripts/tune/ab/libsrcdsp_hip_corrmfma.so
+      SRCDSP_HIP_LIB=$L step corrlib_check_$TAG 300 python -u scripts/tune/corr_mfma_lib.py
+      SRCDSP_HIP_LIB=$L step corrlib_tests_$TAG 900 python -u -m pytest tests -m gpu -q --timeout 120 \
+        --timeout-method thread --maxfail=30 -k "corr or config5 or time_split"
+      SRCDSP_HIP_LIB=$L SRCDSP_CORR_MFMA_PL=2 step corrlib_tests2_$TAG 600 python -u -m pytest \
+        tests/test_gpu_parity.py -m gpu -q --timeout 120 --timeout-method thread -k "config5 or time_split"
+      for rep in 1 2; do
+        sleep ${IDLE:-8}
+        step corrlib_benchprod${rep}_$TAG 300 python -u bench.py --workload corr --no-cpu-baseline --no-pcie --warmup 5 --steps 20
+        sleep ${IDLE:-8}
+        SRCDSP_HIP_LIB=$L step corrlib_bench${rep}_$TAG 300 python -u bench.py --workload corr --no-cpu-baseline --no-pcie \
+          --warmup 5 --steps 20
+        sleep ${IDLE:-8}
+        SRCDSP_HIP_LIB=$L SRCDSP_CORR_MFMA_PL=2 step corrlib_bench2l${rep}_$TAG 300 python -u bench.py --workload corr \
+          --no-cpu-baseline --no-pcie --warmup 5 --steps 20
+      done
+      SRCDSP_HIP_LIB=$L step corrlib_prof_$TAG 300 rocprofv3 --kernel-trace --stats -d gpurun_out/corrlib_prof_$TAG -o run \
+        --output-format csv -- python3 bench.py --workload corr --no-cpu-baseline --no-pcie --warmup 5 --steps 20 ;;
     cpp) step cpp_$TAG 600 python -u -m pytest tests/test_dropin_cpp.py -m gpu -v --timeout 240 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

@@ -19,10 +19,14 @@ scripts/tune/ab_libs.sh (LIBS="<name> new").
            256-lane workgroups (the same 8192-sample tiles and LDS image), 2
            waves per SIMD (the wider window and the doubled per-lane prefetch
            need up to 256 VGPRs)
+  corrmfma the correlator's fused scan (srcdsp_corr_step, N = 1024, S = 1)
+           on the i8 matrix cores behind the product's C ABI
+           (scripts/tune/corr_mfma_scan.h; SRCDSP_CORR_MFMA=0 turns it off at
+           run time, SRCDSP_CORR_MFMA_PL=2 forces two pattern limbs)
   rev:<REV> the product sources of git revision REV, unpatched (e.g. rev:HEAD
            before a kernel change is committed); built as libsrcdsp_hip_<REV>.so
 
-    python scripts/tune/variant_lib.py halflds|r4mix|rev:<REV>
+    python scripts/tune/variant_lib.py halflds|r8|corrmfma|rev:<REV>
 """
 from __future__ import annotations
 
@@ -118,6 +122,45 @@ int launch_cf32(""")
                     } else {""")],
 }
 
+# the correlator's fused scan on the i8 matrix cores (scripts/tune/corr_mfma_scan.h)
+PATCHES["corrmfma"] = [
+    ("corr.hip", "    unsigned *d_best = nullptr;\n",
+     "    unsigned *d_best = nullptr;\n"
+     "    int mfma_pl = 0;             // tuning variant: 1 or 2 pattern limbs, 0 = the product path\n"
+     "    uint32_t mfma_scale = 1, mfma_bias[2] = {0u, 0u};\n"
+     "    unsigned char *d_mfma_b = nullptr;\n"
+     "    uint32_t *d_seams = nullptr;\n"
+     "    size_t seams_cap = 0;\n"),
+    ("corr.hip", "// ---------------------------------------------------------------- host side\n",
+     "#include \"corr_mfma_scan.h\"\n\n// ---------------------------------------------------------------- host side\n"),
+    ("corr.hip", """        hipLaunchKernelGGL(corr_scan_s1, dim3((unsigned)blocks), dim3(kCBlock), smem, s, d_in, n, hist, c.d_ptaps,
+                           (int)c.N, (int)c.NP, cs, c.corr[0], c.corr[1], c.energy[0], c.d_best);
+        SRCDSP_HIP_TRY(hipGetLastError());
+""", """        if (corr_mfma_usable(c, d_in, n)) {
+            rc = corr_mfma_launch(c, d_in, n, hist, s);
+            if (rc) return rc;
+        } else {
+            hipLaunchKernelGGL(corr_scan_s1, dim3((unsigned)blocks), dim3(kCBlock), smem, s, d_in, n, hist, c.d_ptaps,
+                               (int)c.N, (int)c.NP, cs, c.corr[0], c.corr[1], c.energy[0], c.d_best);
+            SRCDSP_HIP_TRY(hipGetLastError());
+        }
+"""),
+    ("corr.hip", "hipMemcpyHostToDevice));\n    return SRCDSP_OK;\n}\n\n// reset",
+     "hipMemcpyHostToDevice));\n    return corr_mfma_prepare(c);\n}\n\n// reset"),
+    ("corr.hip", "    c.cur = 0;\n    *out = n;\n",
+     "    c.cur = 0;\n    rc = corr_mfma_prepare(c);\n    if (rc) {\n        srcdsp_corr_destroy(n);\n"
+     "        return rc;\n    }\n    *out = n;\n"),
+    ("corr.hip", "(void *)c.d_best})", "(void *)c.d_best, (void *)c.d_mfma_b, (void *)c.d_seams})"),
+]
+
+# variants whose patch sites the product sources have since moved past (the
+# A/B they were built for is recorded; rebuild such a baseline with rev:<REV>)
+STALE = {"r4mix": "round 6 moved config 4's mixer table into registers (ccc91a7): build rev:ccc91a7~1 for round 5's "
+                  "side of that A/B"}
+
+# files a variant adds to its csrc copy (from scripts/tune/)
+EXTRA = {"corrmfma": ["corr_mfma_scan.h"]}
+
 
 # extra compiler flags of a variant (the whole library)
 FLAGS = {
@@ -130,6 +173,8 @@ FLAGS = {
 def main():
     name = sys.argv[1]
     rev = name[4:] if name.startswith("rev:") else None
+    if name in STALE:
+        sys.exit(f"{name}: stale ({STALE[name]})")
     out = os.path.join(HERE, "ab", f"libsrcdsp_hip_{rev or name}.so")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     with tempfile.TemporaryDirectory() as d:
@@ -141,6 +186,8 @@ def main():
         else:
             shutil.copytree(B.CSRC, src)
             shutil.copytree(os.path.join(ROOT, "include"), os.path.join(d, "include"))
+        for fname in ([] if rev else EXTRA.get(name, [])):
+            shutil.copy(os.path.join(HERE, fname), src)
         for fname, old, new in ([] if rev else PATCHES[name]):
             k = os.path.join(src, fname)
             text = open(k).read()
