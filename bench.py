@@ -164,7 +164,7 @@ def share_layout(args, world: int, L: int | None = None) -> dict | None:
     total = CONFIG2_PER_GPU * world
     return {"channels_per_gpu": CONFIG2_PER_GPU, "channels_total": total, "samples_per_channel": L,
             "baseline_config": layout_label(CONFIG2_PER_GPU, world),
-            "gather_bytes": total * (L // 4) * 8 if world > 1 else 0}
+            "gather_bytes": total * (L // 4) * 8 if use_pg(world) else 0}
 
 
 def dry_run(args) -> None:
@@ -266,6 +266,15 @@ DEV = None  # set by main(): CudaDevice() unless a HostDevice is passed in
 # collectives then move host copies); its timings are not scaling numbers.
 BACKEND = os.environ.get("SRCDSP_BENCH_BACKEND", "nccl")
 COLL_DEV = "cuda" if BACKEND == "nccl" else None  # device of the collectives' small tensors
+# SRCDSP_BENCH_PG=1: a process group (and every collective of the N > 1 path:
+# barriers, MAX of the wall times, parity SUMs, the share's gather, the
+# correlator's MIN) even at WORLD_SIZE 1 -- the N > 1 path on the real backend
+# on a one-GPU box, as a rehearsal; the line is the same work as N = 1
+FORCE_PG = os.environ.get("SRCDSP_BENCH_PG") == "1"
+
+
+def use_pg(world: int) -> bool:
+    return world > 1 or FORCE_PG
 
 
 def dist_setup(args):
@@ -273,7 +282,7 @@ def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if use_pg(world):
         import torch.distributed as dist
         if BACKEND == "nccl":
             DEV.set_device(local)
@@ -287,7 +296,7 @@ def dist_setup(args):
 
 
 def barrier(world):
-    if world > 1:
+    if use_pg(world):
         import torch.distributed as dist
         dist.barrier()
     DEV.synchronize()
@@ -956,7 +965,7 @@ def gathered_parity(bufs, args, L, table) -> dict:
 def reduce_parity(p: dict, world: int) -> dict:
     """SUM of the per-rank counts over ranks (bad channel ids: rank 0's view
     plus the total count)."""
-    if world > 1:
+    if use_pg(world):
         import torch
         import torch.distributed as dist
         t = torch.tensor([p["channels_checked"], p["mismatches"], p["missing"]], dtype=torch.int64,
@@ -1012,7 +1021,7 @@ def measure_share(S, torch, args, world, rank, L, slay, table=None) -> dict:
     if not args.no_parity:
         # after the timed steps: a fresh step per channel, digests vs the table
         out["parity"] = reduce_parity(channel_parity(work, args, rank, table), world)
-    if world > 1 and not args.no_gather:
+    if use_pg(world) and not args.no_gather:
         barrier(world)
         g0 = time.perf_counter()
         bufs = gather_to_root(work.y if COLL_DEV else work.y.cpu(), world, rank)
@@ -1047,7 +1056,7 @@ def main(argv=None, S=None, dev=None):
     DEV = dev if dev is not None else CudaDevice()
     world, rank, local = dist_setup(args)
     reported = world
-    if world > 1:
+    if use_pg(world):
         import torch.distributed as dist
         reported = dist.get_world_size()  # what the process group (RCCL) actually assembled
     if world != args.gpus or reported != args.gpus:
@@ -1175,7 +1184,7 @@ def main(argv=None, S=None, dev=None):
                 "vs_baseline": None, "dtype": work_dtype,
                 "data": "synthetic (counter-based splitmix64 integer samples, SURVEY §8d)", "config": cfg,
                 "roofline": roof, "hbm_read": hbm_read, "world_size_reported": reported,
-                "backend": BACKEND if world > 1 else None}
+                "backend": BACKEND if use_pg(world) else None}
         if args.workload == "decim":
             # `roofline` is rank 0's own launch(es): per GPU, the same work at every N
             roof["per_gpu"] = True
@@ -1201,7 +1210,7 @@ def main(argv=None, S=None, dev=None):
         print(json.dumps(line), flush=True)
     if hasattr(work, "close"):
         work.close()
-    if world > 1:
+    if use_pg(world):
         import torch.distributed as dist
         dist.destroy_process_group()
 

@@ -32,6 +32,7 @@
 #                    (scripts/tune/corr_mfma.py ${CORR_ARGS}, for each of ${CORR_LIBS}) and config 4's tap loop
 #                    (scripts/tune/mixdecim_mfma.py ${MIX_ARGS}), each checked against the oracle and timed
 #                    beside the product on the same box
+#   pg1              bench.py's N > 1 path at one rank on RCCL (SRCDSP_BENCH_PG=1, launched by torchrun)
 #   corrlib          the correlator's fused scan on the i8 matrix cores behind the product's C ABI (tuning
 #                    library scripts/tune/ab/libsrcdsp_hip_corrmfma.so, never shipped): parity, tests, bench
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -132,6 +133,12 @@ for s in ${STEPS:-smoke tests bench}; do
       done
       SRCDSP_HIP_LIB=$L step corrlib_prof_$TAG 300 rocprofv3 --kernel-trace --stats -d gpurun_out/corrlib_prof_$TAG -o run \
         --output-format csv -- python3 bench.py --workload corr --no-cpu-baseline --no-pcie --warmup 5 --steps 20 ;;
+    pg1)  # the N > 1 path on the real backend at one rank (torchrun, RCCL process group, device collectives,
+          # the share's gather and its digests; bench.py SRCDSP_BENCH_PG=1)
+      SRCDSP_BENCH_PG=1 step pg1_decim_$TAG 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+        --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 1 --share --steps 5 --warmup 2 --no-cpu-baseline --no-pcie
+      SRCDSP_BENCH_PG=1 step pg1_corr_$TAG 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+        --master-addr 127.0.0.1 --master-port 29612 bench.py --gpus 1 --workload corr --steps 5 --warmup 2 --no-cpu-baseline ;;
     cpp) step cpp_$TAG 600 python -u -m pytest tests/test_dropin_cpp.py -m gpu -v --timeout 240 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

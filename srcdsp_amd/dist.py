@@ -19,6 +19,15 @@ over RCCL/xGMI).
 from __future__ import annotations
 
 
+def _single(world: int) -> bool:
+    """world 1 and no process group: nothing to exchange (with a one-rank
+    group -- bench.py's SRCDSP_BENCH_PG rehearsal -- the collectives run)"""
+    if world != 1:
+        return False
+    import torch.distributed as dist
+    return not (dist.is_available() and dist.is_initialized())
+
+
 def channels_for_rank(total_channels: int, world: int, rank: int) -> range:
     """Contiguous block partition; the first total % world ranks get one extra."""
     if not (0 <= rank < world) or total_channels < 0:
@@ -34,7 +43,7 @@ def gather_to_root(t, world: int, rank: int):
     same call runs on CPU tensors."""
     import torch
     import torch.distributed as dist
-    if world == 1:
+    if _single(world):
         return [t]
     cplx = t.is_complex()
     src = torch.view_as_real(t) if cplx else t  # collectives move complex data as real pairs
@@ -49,7 +58,7 @@ def max_over_ranks(x: float, world: int, device=None) -> float:
     """MAX of a host scalar over ranks (the bench's per-rank wall times)."""
     import torch
     import torch.distributed as dist
-    if world == 1:
+    if _single(world):
         return x
     t = torch.tensor([x], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -86,7 +95,7 @@ def first_detection(local_index, world: int, device=None) -> int:
     import torch
     import torch.distributed as dist
     v = NO_DETECTION if local_index is None else int(local_index)
-    if world == 1:
+    if _single(world):
         return v
     t = torch.tensor([v], dtype=torch.int64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MIN)

@@ -187,6 +187,20 @@ def test_bench_main_one_rank_with_share_on_host():
     assert sh["parity"]["channels_checked"] == 8 and "gather_ms" not in sh
 
 
+@pytest.mark.skipif(not os.path.exists(DIGESTS), reason="tests/golden/channel_digests.json not generated")
+def test_bench_main_one_rank_process_group_rehearsal():
+    """SRCDSP_BENCH_PG=1 at one rank: the process group and every N > 1
+    collective (barriers, MAX, parity SUMs, the share's gather, rank 0's
+    gathered digests) run at world 1 -- what the GPU box's one-rank RCCL
+    rehearsal (scripts/gpu_session.sh pg1) executes on the real backend."""
+    line = _host_ranks(1, {"SRCDSP_BENCH_PG": "1"}, args=("--share",))
+    assert line["n_gpus"] == 1 and line["backend"] == "gloo" and line["world_size_reported"] == 1
+    assert line["parity"]["channels_checked"] == 1 and line["parity"]["mismatches"] == 0
+    sh = line["configs2_share"]
+    assert sh["gather_bytes"] == 8 * (1 << 18) * 8 and sh["gather_ms"] > 0
+    assert (sh["gather_parity"]["channels_checked"], sh["gather_parity"]["mismatches"]) == (8, 0)
+
+
 def test_host_leg_reports_a_failure_instead_of_raising():
     def boom(args):
         raise OSError("affinity refused")
