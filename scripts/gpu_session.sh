@@ -32,6 +32,8 @@
 #                    (scripts/tune/corr_mfma.py ${CORR_ARGS}, for each of ${CORR_LIBS}) and config 4's tap loop
 #                    (scripts/tune/mixdecim_mfma.py ${MIX_ARGS}), each checked against the oracle and timed
 #                    beside the product on the same box
+#   mixlib           config 4's chain with its tap loop on the i8 matrix cores behind the product's C ABI (tuning
+#                    library scripts/tune/ab/libsrcdsp_hip_mixmfma.so, never shipped): parity, tests, bench
 #   pg1              bench.py's N > 1 path at one rank on RCCL (SRCDSP_BENCH_PG=1, launched by torchrun)
 #   corrlib          the correlator's fused scan on the i8 matrix cores behind the product's C ABI (tuning
 #                    library scripts/tune/ab/libsrcdsp_hip_corrmfma.so, never shipped): parity, tests, bench
@@ -133,6 +135,26 @@ for s in ${STEPS:-smoke tests bench}; do
       done
       SRCDSP_HIP_LIB=$L step corrlib_prof_$TAG 300 rocprofv3 --kernel-trace --stats -d gpurun_out/corrlib_prof_$TAG -o run \
         --output-format csv -- python3 bench.py --workload corr --no-cpu-baseline --no-pcie --warmup 5 --steps 20 ;;
+    mixlib)  # the mixmfma tuning library behind the product's C ABI: its own cases, the chain GPU tests,
+             # then config 4's bench line beside the product's
+      L=$PWD/scripts/tune/ab/libsrcdsp_hip_mixmfma.so
+      SRCDSP_HIP_LIB=$L step mixlib_check_$TAG 300 python -u scripts/tune/mixdecim_mfma_lib.py
+      SRCDSP_HIP_LIB=$L step mixlib_tests_$TAG 900 python -u -m pytest tests -m gpu -q --timeout 120 \
+        --timeout-method thread --maxfail=30 -k "chain or mixdecim or config4 or mixer or pipeline or streams"
+      for rep in 1 2; do
+        sleep ${IDLE:-8}
+        step mixlib_benchprod${rep}_$TAG 300 python -u bench.py --workload mixdecim --no-cpu-baseline --no-pcie \
+          --warmup 5 --steps 20
+        sleep ${IDLE:-8}
+        SRCDSP_HIP_LIB=$L step mixlib_bench${rep}_$TAG 300 python -u bench.py --workload mixdecim --no-cpu-baseline \
+          --no-pcie --warmup 5 --steps 20
+      done
+      SRCDSP_HIP_LIB=$L step mixlib_steady_$TAG 300 python -u bench.py --workload mixdecim --no-cpu-baseline --no-pcie \
+        --warmup 100 --steps 50
+      step mixlib_steadyprod_$TAG 300 python -u bench.py --workload mixdecim --no-cpu-baseline --no-pcie \
+        --warmup 100 --steps 50
+      SRCDSP_HIP_LIB=$L step mixlib_prof_$TAG 300 rocprofv3 --kernel-trace --stats -d gpurun_out/mixlib_prof_$TAG -o run \
+        --output-format csv -- python3 bench.py --workload mixdecim --no-cpu-baseline --no-pcie --warmup 5 --steps 20 ;;
     pg1)  # the N > 1 path on the real backend at one rank (torchrun, RCCL process group, device collectives,
           # the share's gather and its digests; bench.py SRCDSP_BENCH_PG=1)
       SRCDSP_BENCH_PG=1 step pg1_decim_$TAG 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \

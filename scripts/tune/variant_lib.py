@@ -158,8 +158,19 @@ PATCHES["corrmfma"] = [
 STALE = {"r4mix": "round 6 moved config 4's mixer table into registers (ccc91a7): build rev:ccc91a7~1 for round 5's "
                   "side of that A/B"}
 
+# config 4's mixer -> decimator chain with the tap loop on the i8 matrix cores
+# (scripts/tune/mixdecim_mfma_step.h)
+PATCHES["mixmfma"] = [
+    ("decim.hip", "}  // namespace srcdsp\n\nusing namespace srcdsp;\n",
+     "#include \"mixdecim_mfma_step.h\"\n\n}  // namespace srcdsp\n\nusing namespace srcdsp;\n"),
+    ("decim.hip", "    rc = core_step(f, d_in, n_in, d_out, n_out, s, &m);\n",
+     "    rc = mixmfma_usable(f, m, d_in, n_in, d_out) ? mixmfma_step(f, m, d_in, n_in, d_out, s)\n"
+     "                                                 : SRCDSP_ERR_UNSUPPORTED;\n"
+     "    if (rc == SRCDSP_ERR_UNSUPPORTED) rc = core_step(f, d_in, n_in, d_out, n_out, s, &m);\n"),
+]
+
 # files a variant adds to its csrc copy (from scripts/tune/)
-EXTRA = {"corrmfma": ["corr_mfma_scan.h"]}
+EXTRA = {"corrmfma": ["corr_mfma_scan.h"], "mixmfma": ["mixdecim_mfma_step.h"]}
 
 
 # extra compiler flags of a variant (the whole library)
