@@ -155,6 +155,13 @@ for s in ${STEPS:-smoke tests bench}; do
         --warmup 100 --steps 50
       SRCDSP_HIP_LIB=$L step mixlib_prof_$TAG 300 rocprofv3 --kernel-trace --stats -d gpurun_out/mixlib_prof_$TAG -o run \
         --output-format csv -- python3 bench.py --workload mixdecim --no-cpu-baseline --no-pcie --warmup 5 --steps 20 ;;
+    libpmc)  # MFMA-busy / clock counters of the two C-ABI matrix-core builds' kernels (PMC_PASSES, default MFMA + traffic)
+      SRCDSP_HIP_LIB=$PWD/scripts/tune/ab/libsrcdsp_hip_corrmfma.so PMC_PASSES=${PMC_PASSES:-0,4,5} step libpmc_corr_$TAG 400 \
+        python -u scripts/tune/pmc_cmd.py gpurun_out/libpmc_corr_$TAG.json corr_scan_mfma \
+        -- python3 bench.py --workload corr --no-cpu-baseline --no-parity --warmup 2 --steps 8
+      SRCDSP_HIP_LIB=$PWD/scripts/tune/ab/libsrcdsp_hip_mixmfma.so PMC_PASSES=${PMC_PASSES:-0,4,5} step libpmc_mix_$TAG 400 \
+        python -u scripts/tune/pmc_cmd.py gpurun_out/libpmc_mix_$TAG.json mixdecim_mfma_step_i8 \
+        -- python3 bench.py --workload mixdecim --no-cpu-baseline --no-pcie --no-parity --warmup 2 --steps 8 ;;
     pg1)  # the N > 1 path on the real backend at one rank (torchrun, RCCL process group, device collectives,
           # the share's gather and its digests; bench.py SRCDSP_BENCH_PG=1)
       SRCDSP_BENCH_PG=1 step pg1_decim_$TAG 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \

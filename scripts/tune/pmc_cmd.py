@@ -18,6 +18,10 @@ sys.path.insert(0, HERE)
 from pmc_workload import PASSES  # noqa: E402
 
 MFMA_PASS = ["SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_MFMA", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE"]
+# HBM traffic, one derived counter per pass (FETCH_SIZE takes 3 TCC counters, WRITE_SIZE 2;
+# scripts/pmc_traffic.py applies the gfx950 corrections: read = 2 x FETCH_SIZE x 1024 B,
+# write = WRITE_SIZE x 1024 B)
+TRAFFIC_PASSES = [["FETCH_SIZE"], ["WRITE_SIZE"]]
 
 
 def one(cmd, ksub, counters, tag):
@@ -62,8 +66,8 @@ def main():
     outp, ksub = sys.argv[1], sys.argv[2]
     cmd = sys.argv[sep + 1:]
     r = {}
-    passes = [MFMA_PASS] + PASSES
-    if os.environ.get("PMC_PASSES"):  # e.g. "0": the MFMA pass only
+    passes = [MFMA_PASS] + PASSES + TRAFFIC_PASSES  # indices 0 (MFMA), 1-3 (SQ), 4-5 (traffic)
+    if os.environ.get("PMC_PASSES"):  # e.g. "0": the MFMA pass only; "0,4,5": and the traffic
         passes = [passes[int(i)] for i in os.environ["PMC_PASSES"].split(",")]
     for i, p in enumerate(passes):
         res = one(cmd, ksub, p, f"p{i}")
