@@ -81,6 +81,9 @@ constexpr int NP = 1024;                 // pattern length (config 5)
 #ifndef CORR_WAVES
 #define CORR_WAVES 8                     // waves per workgroup (8: one workgroup per CU)
 #endif
+#ifndef CORR_A_DPP
+#define CORR_A_DPP 0                     // 1: A of chunk t+2 = A of chunk t one row on (DPP wave_shl:1), LDS only for row 31
+#endif
 constexpr int WAVES = CORR_WAVES;
 constexpr int LANES = 64 * WAVES;
 constexpr int TILE = 1024 * WAVES;       // outputs per workgroup tile
@@ -273,6 +276,70 @@ corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ bta
             return f;
         };
         Frags cur = load(0);
+#if CORR_A_DPP
+        // A_{t+2}[row] = A_t[row + 1] (32 (row + 1) + 16 t = 32 row + 16 (t + 2)): the
+        // next-but-one chunk's A fragments are this chunk's one lane on (DPP
+        // wave_shl:1, lane l <- lane l + 1); only row 31 of each lane group (lanes
+        // 31 and 63) reads its 16 bytes from LDS.  Halves the LDS bytes per chunk
+        // with one limb (B stays 2 fragments from LDS).
+        v4i a1l, a1h;
+        {
+            const Frags f1 = load(1);
+            a1l = f1.xl;
+            a1h = f1.xh;
+        }
+        auto shl1 = [](v4i v) {
+            v4i r;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) r[q] = __builtin_amdgcn_update_dpp(0, v[q], 0x130, 0xf, 0xf, false);
+            return r;
+        };
+#pragma unroll 2
+        for (int t = 0; t < CHUNKS; ++t) {
+            const int tb = t + 1 < CHUNKS ? t + 1 : t;
+            const unsigned char* pbt = pb + 32 * tb;
+            v4i nrl = ld_b64x2(pbt), nrh = {}, nil, nih = {};
+            if constexpr (PL == 2) {
+                nrh = ld_b64x2(pbt + BKIND);
+                nil = ld_b64x2(pbt + 2 * BKIND);
+                nih = ld_b64x2(pbt + 3 * BKIND);
+            } else {
+                nil = ld_b64x2(pbt + BKIND);
+            }
+            v4i a2l = shl1(cur.xl), a2h = shl1(cur.xh);
+            if (rc == 31) {
+                const int t2 = t + 2 < CHUNKS ? t + 2 : t;
+                const int g = a_g0 + (t2 >> 1);
+                const int ao = 64 * g + 16 * ((2 * (t2 & 1) + h) ^ ((g >> 2) & 3));
+                a2l = *(const v4i*)(pa + ao);
+                a2h = *(const v4i*)(pa + PLANE + ao);
+            }
+#if CORR_SCHED_BARRIER
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+            s0r = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl, cur.rl, s0r, 0, 0, 0);
+            s0i = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl, cur.il, s0i, 0, 0, 0);
+            if constexpr (PL == 2) {
+                s1r = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl, cur.rh, s1r, 0, 0, 0);
+                s1i = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl, cur.ih, s1i, 0, 0, 0);
+                s2r = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh, cur.rh, s2r, 0, 0, 0);
+                s2i = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh, cur.ih, s2i, 0, 0, 0);
+            }
+            s1r = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh, cur.rl, s1r, 0, 0, 0);
+            s1i = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh, cur.il, s1i, 0, 0, 0);
+#if CORR_SCHED_BARRIER
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+            cur.xl = a1l;
+            cur.xh = a1h;
+            cur.rl = nrl;
+            cur.rh = nrh;
+            cur.il = nil;
+            cur.ih = nih;
+            a1l = a2l;
+            a1h = a2h;
+        }
+#else
 #pragma unroll 2
         for (int t = 0; t < CHUNKS; ++t) {
 #if PROBE_SKIP_A || PROBE_SKIP_B
@@ -311,6 +378,7 @@ corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ bta
             cur = nxt;
 #endif
         }
+#endif  // CORR_A_DPP
 
         // ---- epilogue: D layout col = l & 15.. 31, row = (r & 3) + 8 (r >> 2) + 4 h
         const unsigned es = (unsigned)(cs / 2) & 31u;

@@ -22,6 +22,10 @@
 //   as on the product's fused path.
 // Per-sample HBM traffic is the 4 B input read (no per-sample scratch).
 
+#ifndef CMF_A_DPP
+#define CMF_A_DPP 0
+#endif
+
 namespace cmf {
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v2i __attribute__((ext_vector_type(2)));
@@ -185,9 +189,53 @@ corr_scan_mfma(const uint32_t* __restrict__ x, long n, const uint32_t* __restric
             return f;
         };
         Frags cur = load(0);
+#if CMF_A_DPP
+        // A of chunk t + 2 = A of chunk t one row on (32 (row + 1) + 16 t =
+        // 32 row + 16 (t + 2)): DPP wave_shl:1 (lane l <- lane l + 1), LDS only for
+        // row 31 of each lane group (scripts/tune/corr_mfma.hip CORR_A_DPP)
+        v4i a1l, a1h;
+        {
+            const Frags f1 = load(1);
+            a1l = f1.xl;
+            a1h = f1.xh;
+        }
+        auto shl1 = [](v4i v) {
+            v4i r;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) r[q] = __builtin_amdgcn_update_dpp(0, v[q], 0x130, 0xf, 0xf, false);
+            return r;
+        };
+#endif
 #pragma unroll 2
         for (int t = 0; t < CHUNKS; ++t) {
+#if CMF_A_DPP
+            Frags nxt;
+            {
+                const unsigned char* pbt = pb + 32 * (t + 1 < CHUNKS ? t + 1 : t);
+                nxt.rl = ld_b64x2(pbt);
+                if constexpr (PL == 2) {
+                    nxt.rh = ld_b64x2(pbt + BKIND);
+                    nxt.il = ld_b64x2(pbt + 2 * BKIND);
+                    nxt.ih = ld_b64x2(pbt + 3 * BKIND);
+                } else {
+                    nxt.il = ld_b64x2(pbt + BKIND);
+                }
+                nxt.xl = a1l;
+                nxt.xh = a1h;
+                v4i a2l = shl1(cur.xl), a2h = shl1(cur.xh);
+                if (rc == 31) {
+                    const int t2 = t + 2 < CHUNKS ? t + 2 : t;
+                    const int g = a_g0 + (t2 >> 1);
+                    const int ao = 64 * g + 16 * ((2 * (t2 & 1) + h) ^ ((g >> 2) & 3));
+                    a2l = *(const v4i*)(ldsA + ao);
+                    a2h = *(const v4i*)(ldsA + PLANE + ao);
+                }
+                a1l = a2l;
+                a1h = a2h;
+            }
+#else
             const Frags nxt = load(t + 1 < CHUNKS ? t + 1 : t);
+#endif
             __builtin_amdgcn_sched_barrier(0);
             s0r = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl, cur.rl, s0r, 0, 0, 0);
             s0i = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl, cur.il, s0i, 0, 0, 0);

@@ -169,8 +169,11 @@ PATCHES["mixmfma"] = [
      "    if (rc == SRCDSP_ERR_UNSUPPORTED) rc = core_step(f, d_in, n_in, d_out, n_out, s, &m);\n"),
 ]
 
+# the same with the A fragments of chunk t + 2 made from chunk t's by a DPP lane shift
+PATCHES["corrmfmadpp"] = PATCHES["corrmfma"]
+
 # files a variant adds to its csrc copy (from scripts/tune/)
-EXTRA = {"corrmfma": ["corr_mfma_scan.h"], "mixmfma": ["mixdecim_mfma_step.h"]}
+EXTRA = {"corrmfma": ["corr_mfma_scan.h"], "corrmfmadpp": ["corr_mfma_scan.h"], "mixmfma": ["mixdecim_mfma_step.h"]}
 
 
 # extra compiler flags of a variant (the whole library)
@@ -178,6 +181,7 @@ FLAGS = {
     # the R = 8 tap loop (32 steps x 32 pk_fma) is past the default
     # pragma-unroll threshold: not unrolled, its window goes to scratch
     "r8": ["-mllvm", "-pragma-unroll-threshold=1000000"],
+    "corrmfmadpp": ["-DCMF_A_DPP=1"],
 }
 
 
