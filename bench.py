@@ -1134,6 +1134,10 @@ def main(argv=None, S=None, dev=None):
         else:
             other = valu
         roof = dict(roof, other_bound=other)
+    if args.workload == "mixdecim":
+        # the tap loop on the i8 matrix cores behind this C ABI (tuning build,
+        # never this line's library; north_star keeps the path on vector MACs)
+        roof["mfma_i8_build"] = "scripts/tune/mixdecim_mfma_step.h; profiles/tuning/r06k_mixlib_bench.json"
     if args.workload == "corr":
         # VALU-bound: 1024 complex taps = 4096 int MACs =
         # 2048 v_dot2 lane-ops per scanned sample; the reference scans up to and
@@ -1157,7 +1161,9 @@ def main(argv=None, S=None, dev=None):
                                "unit": "Gsamples/s", "frac": round(rate / i8, 4),
                                "formulation": "int8 limbs of the int16 samples and of the pattern, Toeplitz "
                                               "32x32x32 tiles, 16896 i8 MACs per output (exact mod 2^32)",
-                               "probe": "scripts/tune/corr_mfma.py; profiles/tuning/r06_corr_mfma.json"}
+                               "probe": "scripts/tune/corr_mfma.py; profiles/tuning/r06_corr_mfma.json",
+                               # the same kernel behind this C ABI (tuning build, never this line's library)
+                               "c_abi_build": "scripts/tune/corr_mfma_scan.h; profiles/tuning/r06g_corrlib_bench.json"}
 
     share = None
     if slay is not None:  # beside the main workload's buffers (2.5 GiB): HBM holds both
