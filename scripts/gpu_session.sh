@@ -119,6 +119,7 @@ for s in ${STEPS:-smoke tests bench}; do
               # cases, the correlator GPU tests, then config 5's bench line beside the product's
       L=$PWD/scripts/tune/ab/libsrcdsp_hip_corrmfma.so
       SRCDSP_HIP_LIB=$L step corrlib_check_$TAG 300 python -u scripts/tune/corr_mfma_lib.py
+      SRCDSP_HIP_LIB=$L SRCDSP_CORR_MFMA_RB=1 step corrlib_checkrb1_$TAG 300 python -u scripts/tune/corr_mfma_lib.py
       SRCDSP_HIP_LIB=$L step corrlib_tests_$TAG 900 python -u -m pytest tests -m gpu -q --timeout 120 \
         --timeout-method thread --maxfail=30 -k "corr or config5 or time_split"
       SRCDSP_HIP_LIB=$L SRCDSP_CORR_MFMA_PL=2 step corrlib_tests2_$TAG 600 python -u -m pytest \
@@ -131,6 +132,9 @@ for s in ${STEPS:-smoke tests bench}; do
           --warmup 5 --steps 20
         sleep ${IDLE:-8}
         SRCDSP_HIP_LIB=$L SRCDSP_CORR_MFMA_PL=2 step corrlib_bench2l${rep}_$TAG 300 python -u bench.py --workload corr \
+          --no-cpu-baseline --no-pcie --warmup 5 --steps 20
+        sleep ${IDLE:-8}
+        SRCDSP_HIP_LIB=$L SRCDSP_CORR_MFMA_RB=1 step corrlib_benchrb1${rep}_$TAG 300 python -u bench.py --workload corr \
           --no-cpu-baseline --no-pcie --warmup 5 --steps 20
       done
       SRCDSP_HIP_LIB=$L step corrlib_prof_$TAG 300 rocprofv3 --kernel-trace --stats -d gpurun_out/corrlib_prof_$TAG -o run \

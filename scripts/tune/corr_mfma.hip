@@ -430,6 +430,168 @@ corr_mfma_i8(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ bta
     }
 }
 
+#ifndef CORR_ROWB
+#define CORR_ROWB 1
+#endif
+#if CORR_ROWB == 2
+// CORR_ROWB = 2 (one limb only): each wave owns TWO 32 x 32 output blocks
+// (2048 consecutive outputs), so every B fragment read from LDS feeds two
+// MFMAs (4 A + 2 B fragment reads per 8 MFMAs instead of 4 + 4): a third fewer
+// LDS instructions per MFMA.  Tile 16384 outputs; its A planes and energy
+// prefix take 139 KB of LDS (the two-limb B tables do not fit beside them); no
+// register prefetch of the next tile (that would need 36 more VGPRs beside the
+// 8 accumulators).
+namespace {
+constexpr int RB_TILE = 2048 * WAVES;
+constexpr int RB_SPAN = RB_TILE + NP;
+constexpr int RB_GROUPS = RB_SPAN / 32;
+constexpr int RB_PLANE = RB_GROUPS * 64;
+constexpr int RB_LDS = BBYTES<1> + 2 * RB_PLANE + RB_SPAN * 4 + WAVES * 4;
+static_assert(RB_LDS <= 160 * 1024, "LDS");
+}  // namespace
+
+__global__ void __launch_bounds__(LANES, 1)
+corr_mfma_i8_rb2(const uint32_t* __restrict__ x, long n, const v4u* __restrict__ btab, int cs, uint32_t bias_re,
+                 uint32_t bias_im, uint32_t scale, uint32_t* __restrict__ corr_out, uint32_t* __restrict__ e_out,
+                 long n_tiles, int store_all)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    unsigned char* ldsB = lds;
+    unsigned char* ldsA = lds + BBYTES<1>;
+    uint32_t* ldsP = (uint32_t*)(lds + BBYTES<1> + 2 * RB_PLANE);
+    uint32_t* ldsW = ldsP + RB_SPAN;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, rc = lane & 31;
+    for (int i = tid; i < BBYTES<1> / 16; i += LANES)
+        ((v4u*)ldsB)[i] = btab[i];
+    const int sig = (rc + 1) & 3;
+    const int copy_off[4] = {0, 2360, 4728, 7096};
+    const int b_base = copy_off[sig] + 2 * (8 * h - rc + 31 + sig);
+    constexpr int NG2 = (RB_SPAN / 4 + LANES - 1) / LANES;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)(4 * n), 0x00020000);
+    for (long tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+        const long i0 = tile * RB_TILE;
+        const long j0 = i0 - NP;
+        v4u pre[NG2];
+#pragma unroll
+        for (int k = 0; k < NG2; ++k) {
+            const int g = tid + LANES * k;
+            pre[k] = v4u{0u, 0u, 0u, 0u};
+            if (g < RB_SPAN / 4)
+                pre[k] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(4 * (j0 + 4 * g)), 0, 0));
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < NG2; ++k) {
+            const int g = tid + LANES * k;
+            if (g >= RB_SPAN / 4) continue;  // (continue, not break: the loop must unroll, pre[] in registers)
+            const v4u v = pre[k];
+            const int js = 4 * g;
+            const int off = sample_addr(js);
+            *(v2i*)(ldsA + off) = v2i{(int)(perm(v[1], v[0], 0x06040200u) ^ 0x80808080u),
+                                      (int)(perm(v[3], v[2], 0x06040200u) ^ 0x80808080u)};
+            *(v2i*)(ldsA + RB_PLANE + off) = v2i{(int)perm(v[1], v[0], 0x07050301u), (int)perm(v[3], v[2], 0x07050301u)};
+            v4u p;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int re = (int16_t)(v[q] & 0xFFFFu), im = (int16_t)(v[q] >> 16);
+                p[q] = (uint32_t)re * (uint32_t)re + (uint32_t)im * (uint32_t)im;
+            }
+            *(v4u*)(ldsP + js) = p;
+        }
+        __syncthreads();
+        {
+            // (the lane's running sums are re-read in the second pass: 34 registers of
+            // partial sums would not fit beside the 8 accumulators)
+            constexpr int PER = (RB_SPAN + LANES - 1) / LANES;
+            uint32_t s = 0;
+            for (int q = 0; q < PER; ++q)
+                if (RB_SPAN % LANES == 0 || PER * tid + q < RB_SPAN) s += ldsP[PER * tid + q];
+            uint32_t incl = s;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t o = __shfl_up(incl, d, 64);
+                if (lane >= d) incl += o;
+            }
+            if (lane == 63) ldsW[w] = incl;
+            __syncthreads();
+            uint32_t base = incl - s;
+            for (int q = 0; q < w; ++q) base += ldsW[q];
+            for (int q = 0; q < PER; ++q)
+                if (RB_SPAN % LANES == 0 || PER * tid + q < RB_SPAN) {
+                    base += ldsP[PER * tid + q];
+                    ldsP[PER * tid + q] = base;
+                }
+        }
+        __syncthreads();
+        v16i s0r[2] = {}, s1r[2] = {}, s0i[2] = {}, s1i[2] = {};
+        const unsigned char* pb = ldsB + b_base;
+        struct F { v4i xl[2], xh[2], rl, il; };
+        auto load = [&](int t) {
+            F f;
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const int g = 32 * (2 * w + b) + rc + (t >> 1);
+                const int ao = 64 * g + 16 * ((2 * (t & 1) + h) ^ ((g >> 2) & 3));
+                f.xl[b] = *(const v4i*)(ldsA + ao);
+                f.xh[b] = *(const v4i*)(ldsA + RB_PLANE + ao);
+            }
+            f.rl = ld_b64x2(pb + 32 * t);
+            f.il = ld_b64x2(pb + BKIND + 32 * t);
+            return f;
+        };
+        F cur = load(0);
+#pragma unroll 2
+        for (int t = 0; t < CHUNKS; ++t) {
+            const F nxt = load(t + 1 < CHUNKS ? t + 1 : t);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                s0r[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl[b], cur.rl, s0r[b], 0, 0, 0);
+                s0i[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl[b], cur.il, s0i[b], 0, 0, 0);
+                s1r[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh[b], cur.rl, s1r[b], 0, 0, 0);
+                s1i[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh[b], cur.il, s1i[b], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            cur = nxt;
+        }
+        const unsigned es = (unsigned)(cs / 2) & 31u;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const long iw = i0 + 2048 * w + 1024 * b;
+            const bool full = iw + 1024 <= n;
+            uint32_t ew[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int li = 2048 * w + 1024 * b + 32 * row + rc + NP;
+                ew[r] = ldsP[li] - ldsP[li - NP];
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int o = 32 * row + rc;
+                const uint32_t cr = scale * ((uint32_t)s0r[b][r] + ((uint32_t)s1r[b][r] << 8) + bias_re);
+                const uint32_t ci = scale * ((uint32_t)s0i[b][r] + ((uint32_t)s1i[b][r] << 8) + bias_im);
+                const int sh = (cs & 31) + 2;
+                const int32_t tr = (((int32_t)cr >> sh) << 8) >> 8;
+                const int32_t ti = (((int32_t)ci >> sh) << 8) >> 8;
+                const uint32_t corr = (uint32_t)(tr * tr) + (uint32_t)(ti * ti);
+                const uint32_t e = ew[r] >> es;
+                if (store_all) {
+                    if (full || iw + o < n) {
+                        corr_out[iw + o] = corr;
+                        e_out[iw + o] = e;
+                    }
+                } else if ((corr & e) == 0xFFFFFFFFu) {
+                    corr_out[iw + o] = corr;
+                    e_out[iw + o] = e;
+                }
+            }
+        }
+    }
+}
+#endif  // CORR_ROWB == 2
+
 extern "C" int tune_corr_mfma_geometry(int* out)
 {
     out[0] = TILE; out[1] = CHUNKS; out[2] = BENT; out[3] = BSTRIDE; out[4] = BKIND; out[5] = BBYTES<2>;
@@ -465,6 +627,24 @@ extern "C" int tune_corr_mfma(const void* x, long n, const void* btab, int cs, u
                               void* corr_out, void* e_out, int grid, int store_all, int pattern_limbs, uint32_t scale,
                               hipStream_t s)
 {
+#if CORR_ROWB == 2
+    if (pattern_limbs != 1) return 3;  // the two-limb B tables do not fit beside the 16 k-output tile
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)corr_mfma_i8_rb2, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           RB_LDS);
+        if (e != hipSuccess) return (int)e;
+        attr = true;
+    }
+    if (n % 4 != 0 || 4 * n >= (1l << 31)) return 1;
+    if (cs < 7 || cs > 29) return 2;
+    const long n_tiles = (n + RB_TILE - 1) / RB_TILE;
+    if (grid <= 0) grid = 256;
+    if (grid > n_tiles) grid = (int)n_tiles;
+    hipLaunchKernelGGL(corr_mfma_i8_rb2, dim3(grid), dim3(LANES), RB_LDS, s, (const uint32_t*)x, n, (const v4u*)btab,
+                       cs, bias_re, bias_im, scale, (uint32_t*)corr_out, (uint32_t*)e_out, n_tiles, store_all);
+    return (int)hipGetLastError();
+#endif
     if (pattern_limbs == 1)
         return launch<1>(x, n, btab, cs, bias_re, bias_im, scale, corr_out, e_out, grid, store_all, s);
     return launch<2>(x, n, btab, cs, bias_re, bias_im, 1u, corr_out, e_out, grid, store_all, s);

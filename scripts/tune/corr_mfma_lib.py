@@ -87,9 +87,11 @@ def main():
         amp = 2 if pn.startswith("qpsk") else 1
         noise_seed = 11 if pn.startswith("qpsk") else 12
         cases = {
-            # peaks on tile seams of one call: outputs 0, 1, 2 of tiles 1..3 and the last tile
-            "seams_one_call": (stream(p, 6 * TILE, [TILE, 2 * TILE + 1, 3 * TILE + 2, 5 * TILE + 1], amp, noise_seed),
-                               [6 * TILE]),
+            # detections on tile seams of one call: outputs 0, 1, 2 of 8192-output tiles (one
+            # row block per wave) and of 16384-output tiles (two: 4 TILE, 6 TILE + 1, 8 TILE + 2)
+            "seams_one_call": (stream(p, 10 * TILE, [TILE, 2 * TILE + 1, 3 * TILE + 2, 4 * TILE, 5 * TILE + 1,
+                                                     6 * TILE + 1, 8 * TILE + 2], amp, noise_seed),
+                               [10 * TILE]),
             # peaks at outputs 0 and 1 of a continued call (the seam on the registers of the call before)
             "seam_call_start": (stream(p, 8 * TILE, [3 * TILE, 5 * TILE + 1], amp, noise_seed + 1),
                                 [3 * TILE, 2 * TILE, 3 * TILE]),

@@ -21,10 +21,10 @@
 //   hit past it matters); the registers after the call come from corr_point,
 //   as on the product's fused path.
 // Per-sample HBM traffic is the 4 B input read (no per-sample scratch).
-
-#ifndef CMF_A_DPP
-#define CMF_A_DPP 0
-#endif
+// * one limb: each wave owns two 32 x 32 output blocks (RB = 2, 16 k-output
+//   tiles), so each B fragment read feeds two MFMAs (the probe's CORR_ROWB = 2:
+//   -8 %); two limbs keep one block per wave (their B tables leave no LDS for
+//   the larger tile).
 
 namespace cmf {
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -35,22 +35,22 @@ typedef unsigned v4u __attribute__((ext_vector_type(4)));
 constexpr int NP = 1024;
 constexpr int WAVES = 8;
 constexpr int LANES = 64 * WAVES;
-constexpr int TILE = 1024 * WAVES;
-constexpr int SPAN = TILE + NP;
-constexpr int GROUPS = SPAN / 32;
-constexpr int PLANE = GROUPS * 64;
 constexpr int CHUNKS = (NP + 32) / 16;
 constexpr int BENT = 1096;
 constexpr int BSTRIDE = 2 * BENT;
 constexpr int BKIND = 7096 + BSTRIDE;
 constexpr int COPY_OFF[4] = {0, 2360, 4728, 7096};
 template <int PL> constexpr int BBYTES = 2 * PL * BKIND;
-constexpr int LDS_A = 2 * PLANE;
-constexpr int LDS_P = SPAN * 4;
-template <int PL> constexpr int LDS_TOTAL = BBYTES<PL> + LDS_A + LDS_P + 16 * 4;
+// RB = output row blocks (32 x 32) per wave: 1, or 2 (one limb only: each B
+// fragment read feeds two MFMAs; the 16 k-output tile's planes and prefix take
+// 139 KB of LDS, no room for the two-limb B tables)
+template <int RB> constexpr int TILE = 1024 * WAVES * RB;
+template <int RB> constexpr int SPAN = TILE<RB> + NP;
+template <int RB> constexpr int PLANE = SPAN<RB> / 32 * 64;
+template <int PL, int RB> constexpr int LDS_TOTAL = BBYTES<PL> + 2 * PLANE<RB> + 4 * SPAN<RB> + 16 * 4;
 constexpr int SEAM_WORDS = 8;
-static_assert(4 * TILE <= LDS_A && 4 * TILE <= LDS_P, "corr / energy words reuse the A planes and the prefix");
-static_assert(LDS_TOTAL<2> <= 160 * 1024, "LDS");
+static_assert(4 * TILE<2> <= 2 * PLANE<2> && 4 * TILE<1> <= 2 * PLANE<1>, "corr words reuse the A planes");
+static_assert(LDS_TOTAL<2, 1> <= 160 * 1024 && LDS_TOTAL<1, 2> <= 160 * 1024, "LDS");
 
 __device__ __forceinline__ int sample_addr(int js)
 {
@@ -65,18 +65,20 @@ __device__ __forceinline__ v4i ld_b64x2(const unsigned char* p)
 }
 }  // namespace cmf
 
-template <int PL>
+template <int PL, int RB>
 __global__ void __launch_bounds__(cmf::LANES, 1)
 corr_scan_mfma(const uint32_t* __restrict__ x, long n, const uint32_t* __restrict__ hist,
                const cmf::v4u* __restrict__ btab, int cs, uint32_t bias_re, uint32_t bias_im, uint32_t scale,
                uint32_t* __restrict__ seams, unsigned* best)
 {
     using namespace cmf;
+    static_assert(RB == 1 || PL == 1, "two row blocks per wave: one limb only");
+    constexpr int T = TILE<RB>, SP = SPAN<RB>, PLN = PLANE<RB>;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     unsigned char* ldsB = lds;
     unsigned char* ldsA = lds + BBYTES<PL>;
-    uint32_t* ldsP = (uint32_t*)(lds + BBYTES<PL> + LDS_A);
-    uint32_t* ldsW = ldsP + SPAN;  // per-wave scan totals, then the stop word
+    uint32_t* ldsP = (uint32_t*)(lds + BBYTES<PL> + 2 * PLN);
+    uint32_t* ldsW = ldsP + SP;        // per-wave scan totals, then the stop word
     uint32_t* ldsC = (uint32_t*)ldsA;  // the tile's corr words (after the MFMAs)
 
     const int tid = threadIdx.x;
@@ -84,24 +86,26 @@ corr_scan_mfma(const uint32_t* __restrict__ x, long n, const uint32_t* __restric
     const int w = tid >> 6;
     const int h = lane >> 5;
     const int rc = lane & 31;
-    const long n_tiles = (n + TILE - 1) / TILE;
+    const long n_tiles = (n + T - 1) / T;
 
     for (int i = tid; i < BBYTES<PL> / 16; i += LANES)
         ((v4u*)ldsB)[i] = btab[i];
-    const int a_g0 = 32 * w + rc;
     const int sig = (rc + 1) & 3;
     const int b_base = COPY_OFF[sig] + 2 * (8 * h - rc + 31 + sig);
 
-    constexpr int NG = (SPAN / 4 + LANES - 1) / LANES;
+    // RB = 1: the next tile's input is fetched into registers before this
+    // tile's MFMAs; RB = 2: at the tile's start (no VGPRs for a prefetch beside
+    // the 8 accumulators)
+    constexpr int NG = (SP / 4 + LANES - 1) / LANES;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)(4 * n), 0x00020000);
     v4u pre[NG];
     auto fetch = [&](long tile) {
-        const long j0 = tile * TILE - NP;
+        const long j0 = tile * T - NP;
 #pragma unroll
         for (int k = 0; k < NG; ++k) {
             const int g = tid + LANES * k;
             pre[k] = v4u{0u, 0u, 0u, 0u};
-            if (g < SPAN / 4) {
+            if (g < SP / 4) {
                 const long j = j0 + 4 * g;
                 if (j >= 0) {  // past the end: the descriptor's range check returns zeros
                     pre[k] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(4 * j), 0, 0));
@@ -113,17 +117,18 @@ corr_scan_mfma(const uint32_t* __restrict__ x, long n, const uint32_t* __restric
             }
         }
     };
-    if (blockIdx.x < n_tiles) fetch(blockIdx.x);
+    if (RB == 1 && blockIdx.x < n_tiles) fetch(blockIdx.x);
 
     for (long tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-        const long i0 = tile * TILE;
+        const long i0 = tile * T;
         if (tid == 0) ldsW[WAVES] = __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();  // previous tile's readers are done; the stop word is visible
         if ((long)ldsW[WAVES] < i0) break;  // a hit before this tile: nothing here can be the first
+        if constexpr (RB == 2) fetch(tile);
 #pragma unroll
         for (int k = 0; k < NG; ++k) {
             const int g = tid + LANES * k;
-            if (g >= SPAN / 4) break;
+            if (g >= SP / 4) continue;  // (not break: the loop must unroll, pre[] stays in registers)
             const v4u v = pre[k];
             const int js = 4 * g;
             const int off = sample_addr(js);
@@ -132,7 +137,7 @@ corr_scan_mfma(const uint32_t* __restrict__ x, long n, const uint32_t* __restric
             const uint32_t hi0 = __builtin_amdgcn_perm(v[1], v[0], 0x07050301u);
             const uint32_t hi1 = __builtin_amdgcn_perm(v[3], v[2], 0x07050301u);
             *(v2i*)(ldsA + off) = v2i{(int)lo0, (int)lo1};
-            *(v2i*)(ldsA + PLANE + off) = v2i{(int)hi0, (int)hi1};
+            *(v2i*)(ldsA + PLN + off) = v2i{(int)hi0, (int)hi1};
             v4u p;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -142,15 +147,15 @@ corr_scan_mfma(const uint32_t* __restrict__ x, long n, const uint32_t* __restric
             *(v4u*)(ldsP + js) = p;
         }
         __syncthreads();
-        if (tile + gridDim.x < n_tiles) fetch(tile + gridDim.x);
-        {
-            constexpr int PER = (SPAN + LANES - 1) / LANES;
-            uint32_t loc[PER];
+        if (RB == 1 && tile + gridDim.x < n_tiles) fetch(tile + gridDim.x);
+        {   // energy: inclusive prefix of |x|^2 over the span
+            constexpr int PER = (SP + LANES - 1) / LANES;
             uint32_t s = 0;
+            uint32_t loc[RB == 1 ? PER : 1];  // RB = 2: the running sums are re-read instead
 #pragma unroll
             for (int q = 0; q < PER; ++q) {
-                if (SPAN % LANES == 0 || PER * tid + q < SPAN) s += ldsP[PER * tid + q];
-                loc[q] = s;
+                if (SP % LANES == 0 || PER * tid + q < SP) s += ldsP[PER * tid + q];
+                if constexpr (RB == 1) loc[q] = s;
             }
             uint32_t incl = s;
 #pragma unroll
@@ -164,19 +169,30 @@ corr_scan_mfma(const uint32_t* __restrict__ x, long n, const uint32_t* __restric
             for (int q = 0; q < w; ++q) base += ldsW[q];
 #pragma unroll
             for (int q = 0; q < PER; ++q)
-                if (SPAN % LANES == 0 || PER * tid + q < SPAN) ldsP[PER * tid + q] = loc[q] + base;
+                if (SP % LANES == 0 || PER * tid + q < SP) {
+                    if constexpr (RB == 1) {
+                        ldsP[PER * tid + q] = loc[q] + base;
+                    } else {
+                        base += ldsP[PER * tid + q];
+                        ldsP[PER * tid + q] = base;
+                    }
+                }
         }
         __syncthreads();
 
-        v16i s0r = {}, s1r = {}, s2r = {}, s0i = {}, s1i = {}, s2i = {};
+        // ---- correlation: wave w owns row blocks RB w .. RB w + RB - 1 (1024 outputs each)
+        v16i s0r[RB] = {}, s1r[RB] = {}, s2r[RB] = {}, s0i[RB] = {}, s1i[RB] = {}, s2i[RB] = {};
         const unsigned char* pb = ldsB + b_base;
-        struct Frags { v4i xl, xh, rl, rh, il, ih; };
+        struct Frags { v4i xl[RB], xh[RB], rl, rh, il, ih; };
         auto load = [&](int t) {
             Frags f;
-            const int g = a_g0 + (t >> 1);
-            const int ao = 64 * g + 16 * ((2 * (t & 1) + h) ^ ((g >> 2) & 3));
-            f.xl = *(const v4i*)(ldsA + ao);
-            f.xh = *(const v4i*)(ldsA + PLANE + ao);
+#pragma unroll
+            for (int b = 0; b < RB; ++b) {
+                const int g = 32 * (RB * w + b) + rc + (t >> 1);
+                const int ao = 64 * g + 16 * ((2 * (t & 1) + h) ^ ((g >> 2) & 3));
+                f.xl[b] = *(const v4i*)(ldsA + ao);
+                f.xh[b] = *(const v4i*)(ldsA + PLN + ao);
+            }
             const int bo = 32 * t;
             f.rl = ld_b64x2(pb + bo);
             if constexpr (PL == 2) {
@@ -189,110 +205,74 @@ corr_scan_mfma(const uint32_t* __restrict__ x, long n, const uint32_t* __restric
             return f;
         };
         Frags cur = load(0);
-#if CMF_A_DPP
-        // A of chunk t + 2 = A of chunk t one row on (32 (row + 1) + 16 t =
-        // 32 row + 16 (t + 2)): DPP wave_shl:1 (lane l <- lane l + 1), LDS only for
-        // row 31 of each lane group (scripts/tune/corr_mfma.hip CORR_A_DPP)
-        v4i a1l, a1h;
-        {
-            const Frags f1 = load(1);
-            a1l = f1.xl;
-            a1h = f1.xh;
-        }
-        auto shl1 = [](v4i v) {
-            v4i r;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) r[q] = __builtin_amdgcn_update_dpp(0, v[q], 0x130, 0xf, 0xf, false);
-            return r;
-        };
-#endif
 #pragma unroll 2
         for (int t = 0; t < CHUNKS; ++t) {
-#if CMF_A_DPP
-            Frags nxt;
-            {
-                const unsigned char* pbt = pb + 32 * (t + 1 < CHUNKS ? t + 1 : t);
-                nxt.rl = ld_b64x2(pbt);
-                if constexpr (PL == 2) {
-                    nxt.rh = ld_b64x2(pbt + BKIND);
-                    nxt.il = ld_b64x2(pbt + 2 * BKIND);
-                    nxt.ih = ld_b64x2(pbt + 3 * BKIND);
-                } else {
-                    nxt.il = ld_b64x2(pbt + BKIND);
-                }
-                nxt.xl = a1l;
-                nxt.xh = a1h;
-                v4i a2l = shl1(cur.xl), a2h = shl1(cur.xh);
-                if (rc == 31) {
-                    const int t2 = t + 2 < CHUNKS ? t + 2 : t;
-                    const int g = a_g0 + (t2 >> 1);
-                    const int ao = 64 * g + 16 * ((2 * (t2 & 1) + h) ^ ((g >> 2) & 3));
-                    a2l = *(const v4i*)(ldsA + ao);
-                    a2h = *(const v4i*)(ldsA + PLANE + ao);
-                }
-                a1l = a2l;
-                a1h = a2h;
-            }
-#else
             const Frags nxt = load(t + 1 < CHUNKS ? t + 1 : t);
-#endif
             __builtin_amdgcn_sched_barrier(0);
-            s0r = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl, cur.rl, s0r, 0, 0, 0);
-            s0i = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl, cur.il, s0i, 0, 0, 0);
-            if constexpr (PL == 2) {
-                s1r = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl, cur.rh, s1r, 0, 0, 0);
-                s1i = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl, cur.ih, s1i, 0, 0, 0);
-                s2r = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh, cur.rh, s2r, 0, 0, 0);
-                s2i = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh, cur.ih, s2i, 0, 0, 0);
+#pragma unroll
+            for (int b = 0; b < RB; ++b) {
+                s0r[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl[b], cur.rl, s0r[b], 0, 0, 0);
+                s0i[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl[b], cur.il, s0i[b], 0, 0, 0);
+                if constexpr (PL == 2) {
+                    s1r[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl[b], cur.rh, s1r[b], 0, 0, 0);
+                    s1i[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xl[b], cur.ih, s1i[b], 0, 0, 0);
+                    s2r[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh[b], cur.rh, s2r[b], 0, 0, 0);
+                    s2i[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh[b], cur.ih, s2i[b], 0, 0, 0);
+                }
+                s1r[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh[b], cur.rl, s1r[b], 0, 0, 0);
+                s1i[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh[b], cur.il, s1i[b], 0, 0, 0);
             }
-            s1r = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh, cur.rl, s1r, 0, 0, 0);
-            s1i = __builtin_amdgcn_mfma_i32_32x32x32_i8(cur.xh, cur.il, s1i, 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
             cur = nxt;
         }
 
         // corr (correlators.h:233-250 via scale32, dsp_complex.cpp:43-46) and
-        // energy words of the wave's 1024 outputs, D layout row = (r & 3) +
-        // 8 (r >> 2) + 4 h, col = rc
+        // energy words of the wave's outputs, D layout row = (r & 3) + 8 (r >> 2)
+        // + 4 h, col = rc, in block b at tile output 1024 (RB w + b)
         const unsigned es = (unsigned)(cs / 2) & 31u;
-        uint32_t cv[16], ev[16];
+        uint32_t cv[RB][16], ev[RB][16];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-            const int li = 1024 * w + 32 * row + rc + NP;
-            ev[r] = (ldsP[li] - ldsP[li - NP]) >> es;
-        }
+        for (int b = 0; b < RB; ++b) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            uint32_t cr, ci;
-            if constexpr (PL == 2) {
-                cr = (uint32_t)s0r[r] + ((uint32_t)s1r[r] << 8) + ((uint32_t)s2r[r] << 16) + bias_re;
-                ci = (uint32_t)s0i[r] + ((uint32_t)s1i[r] << 8) + ((uint32_t)s2i[r] << 16) + bias_im;
-            } else {
-                cr = scale * ((uint32_t)s0r[r] + ((uint32_t)s1r[r] << 8) + bias_re);
-                ci = scale * ((uint32_t)s0i[r] + ((uint32_t)s1i[r] << 8) + bias_im);
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int li = 1024 * (RB * w + b) + 32 * row + rc + NP;
+                ev[b][r] = (ldsP[li] - ldsP[li - NP]) >> es;
             }
-            const int sh = (cs & 31) + 2;
-            const int32_t tr = (((int32_t)cr >> sh) << 8) >> 8;
-            const int32_t ti = (((int32_t)ci >> sh) << 8) >> 8;
-            cv[r] = (uint32_t)(tr * tr) + (uint32_t)(ti * ti);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                uint32_t cr, ci;
+                if constexpr (PL == 2) {
+                    cr = (uint32_t)s0r[b][r] + ((uint32_t)s1r[b][r] << 8) + ((uint32_t)s2r[b][r] << 16) + bias_re;
+                    ci = (uint32_t)s0i[b][r] + ((uint32_t)s1i[b][r] << 8) + ((uint32_t)s2i[b][r] << 16) + bias_im;
+                } else {
+                    cr = scale * ((uint32_t)s0r[b][r] + ((uint32_t)s1r[b][r] << 8) + bias_re);
+                    ci = scale * ((uint32_t)s0i[b][r] + ((uint32_t)s1i[b][r] << 8) + bias_im);
+                }
+                const int sh = (cs & 31) + 2;
+                const int32_t tr = (((int32_t)cr >> sh) << 8) >> 8;
+                const int32_t ti = (((int32_t)ci >> sh) << 8) >> 8;
+                cv[b][r] = (uint32_t)(tr * tr) + (uint32_t)(ti * ti);
+            }
         }
         __syncthreads();  // every wave is done with the A planes and the prefix
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-            const int o = 1024 * w + 32 * row + rc;
-            ldsC[o] = cv[r];
-            ldsP[o] = ev[r];
-        }
+        for (int b = 0; b < RB; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int o = 1024 * (RB * w + b) + 32 * row + rc;
+                ldsC[o] = cv[b][r];
+                ldsP[o] = ev[b][r];
+            }
         __syncthreads();
         // the 3-point test (correlators.h:262-268) of tile outputs o >= 2,
-        // o = 1024 w + 64 q + lane: consecutive lanes read consecutive words
+        // o = 1024 RB w + 64 q + lane: consecutive lanes read consecutive words
         const long nrem = n - i0;
         int hit = -1;
 #pragma unroll 4
-        for (int q = 0; q < 16; ++q) {
-            const int o = 1024 * w + 64 * q + lane;
+        for (int q = 0; q < 16 * RB; ++q) {
+            const int o = 1024 * RB * w + 64 * q + lane;
             if (o >= 2 && o < nrem && corr_hit(ldsC[o - 2], ldsC[o - 1], ldsC[o], ldsP[o - 1])) {
                 hit = o;
                 break;
@@ -300,7 +280,7 @@ corr_scan_mfma(const uint32_t* __restrict__ x, long n, const uint32_t* __restric
         }
         if (hit >= 0) atomicMin(best, (unsigned)(i0 + hit));
         if (tid < 6) {  // the seam words: corr[0], corr[1], en[0], corr[T-2], corr[T-1], en[T-1]
-            const int src[6] = {0, 1, 0, TILE - 2, TILE - 1, TILE - 1};
+            const int src[6] = {0, 1, 0, T - 2, T - 1, T - 1};
             const uint32_t v = (tid == 2 || tid == 5) ? ldsP[src[tid]] : ldsC[src[tid]];
             seams[SEAM_WORDS * tile + tid] = v;
         }
@@ -310,13 +290,13 @@ corr_scan_mfma(const uint32_t* __restrict__ x, long n, const uint32_t* __restric
 // the first two outputs of every scanned tile, from the seam words of the tile
 // and of the one before it (tile 0: the registers from before the call, as
 // corr_detect's c_prev0 / c_prev1 / e_prev0)
-__global__ void corr_mfma_seams(const uint32_t* __restrict__ seams, long n, uint32_t c_prev0, uint32_t c_prev1,
-                                uint32_t e_prev0, unsigned* best)
+__global__ void corr_mfma_seams(const uint32_t* __restrict__ seams, long n, long tile_outputs, uint32_t c_prev0,
+                                uint32_t c_prev1, uint32_t e_prev0, unsigned* best)
 {
-    const long n_tiles = (n + cmf::TILE - 1) / cmf::TILE;
+    const long n_tiles = (n + tile_outputs - 1) / tile_outputs;
     const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n_tiles) return;
-    const long i0 = t * cmf::TILE;
+    const long i0 = t * tile_outputs;
     if ((long)__hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < i0) return;  // not scanned
     const uint32_t* s = seams + cmf::SEAM_WORDS * t;
     uint32_t pc2 = c_prev1, pc1 = c_prev0, pe1 = e_prev0;  // corr[i0-2], corr[i0-1], en[i0-1]
@@ -424,18 +404,18 @@ static bool corr_mfma_usable(const srcdsp_corr_state& c, const uint32_t* d_in, l
            ((uintptr_t)d_in & 15) == 0;
 }
 
-template <int PL>
+template <int PL, int RB>
 static int corr_mfma_launch_t(srcdsp_corr_state& c, const uint32_t* d_in, long n, const uint32_t* hist,
                               hipStream_t s)
 {
     using namespace cmf;
     static bool attr = false;
     if (!attr) {
-        SRCDSP_HIP_TRY(hipFuncSetAttribute((const void*)corr_scan_mfma<PL>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           LDS_TOTAL<PL>));
+        SRCDSP_HIP_TRY(hipFuncSetAttribute((const void*)corr_scan_mfma<PL, RB>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, LDS_TOTAL<PL, RB>));
         attr = true;
     }
-    const long n_tiles = (n + TILE - 1) / TILE;
+    const long n_tiles = (n + TILE<RB> - 1) / TILE<RB>;
     if ((size_t)n_tiles > c.seams_cap) {
         if (c.d_seams) (void)hipFree(c.d_seams);
         c.d_seams = nullptr;
@@ -444,12 +424,12 @@ static int corr_mfma_launch_t(srcdsp_corr_state& c, const uint32_t* d_in, long n
         c.seams_cap = (size_t)n_tiles;
     }
     const int grid = (int)std::min<long>(256, n_tiles);
-    hipLaunchKernelGGL(corr_scan_mfma<PL>, dim3(grid), dim3(LANES), LDS_TOTAL<PL>, s, d_in, n, hist,
+    hipLaunchKernelGGL((corr_scan_mfma<PL, RB>), dim3(grid), dim3(LANES), (LDS_TOTAL<PL, RB>), s, d_in, n, hist,
                        (const v4u*)c.d_mfma_b, c.coeff_scaling, c.mfma_bias[0], c.mfma_bias[1], c.mfma_scale,
                        c.d_seams, c.d_best);
     SRCDSP_HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(corr_mfma_seams, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, s,
-                       (const uint32_t*)c.d_seams, n, c.corr[0], c.corr[1], c.energy[0], c.d_best);
+                       (const uint32_t*)c.d_seams, n, (long)TILE<RB>, c.corr[0], c.corr[1], c.energy[0], c.d_best);
     SRCDSP_HIP_TRY(hipGetLastError());
     return SRCDSP_OK;
 }
@@ -461,5 +441,9 @@ extern "C" __attribute__((visibility("default"))) long srcdsp_tune_corr_mfma_lau
 static int corr_mfma_launch(srcdsp_corr_state& c, const uint32_t* d_in, long n, const uint32_t* hist, hipStream_t s)
 {
     ++g_corr_mfma_launches;
-    return c.mfma_pl == 1 ? corr_mfma_launch_t<1>(c, d_in, n, hist, s) : corr_mfma_launch_t<2>(c, d_in, n, hist, s);
+    if (c.mfma_pl == 2) return corr_mfma_launch_t<2, 1>(c, d_in, n, hist, s);
+    // one limb: two row blocks per wave unless SRCDSP_CORR_MFMA_RB=1 (A/B)
+    const char* rb = getenv("SRCDSP_CORR_MFMA_RB");
+    if (rb && rb[0] == '1') return corr_mfma_launch_t<1, 1>(c, d_in, n, hist, s);
+    return corr_mfma_launch_t<1, 2>(c, d_in, n, hist, s);
 }

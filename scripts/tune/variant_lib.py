@@ -22,7 +22,11 @@ scripts/tune/ab_libs.sh (LIBS="<name> new").
   corrmfma the correlator's fused scan (srcdsp_corr_step, N = 1024, S = 1)
            on the i8 matrix cores behind the product's C ABI
            (scripts/tune/corr_mfma_scan.h; SRCDSP_CORR_MFMA=0 turns it off at
-           run time, SRCDSP_CORR_MFMA_PL=2 forces two pattern limbs)
+           run time, SRCDSP_CORR_MFMA_PL=2 forces two pattern limbs,
+           SRCDSP_CORR_MFMA_RB=1 one row block per wave with one limb)
+  mixmfma  config 4's mixer -> decimator chain with the tap loop on the i8
+           matrix cores behind srcdsp_mixdecim_step
+           (scripts/tune/mixdecim_mfma_step.h; SRCDSP_MIXDECIM_MFMA=0: off)
   rev:<REV> the product sources of git revision REV, unpatched (e.g. rev:HEAD
            before a kernel change is committed); built as libsrcdsp_hip_<REV>.so
 
@@ -169,11 +173,8 @@ PATCHES["mixmfma"] = [
      "    if (rc == SRCDSP_ERR_UNSUPPORTED) rc = core_step(f, d_in, n_in, d_out, n_out, s, &m);\n"),
 ]
 
-# the same with the A fragments of chunk t + 2 made from chunk t's by a DPP lane shift
-PATCHES["corrmfmadpp"] = PATCHES["corrmfma"]
-
 # files a variant adds to its csrc copy (from scripts/tune/)
-EXTRA = {"corrmfma": ["corr_mfma_scan.h"], "corrmfmadpp": ["corr_mfma_scan.h"], "mixmfma": ["mixdecim_mfma_step.h"]}
+EXTRA = {"corrmfma": ["corr_mfma_scan.h"], "mixmfma": ["mixdecim_mfma_step.h"]}
 
 
 # extra compiler flags of a variant (the whole library)
@@ -181,7 +182,6 @@ FLAGS = {
     # the R = 8 tap loop (32 steps x 32 pk_fma) is past the default
     # pragma-unroll threshold: not unrolled, its window goes to scratch
     "r8": ["-mllvm", "-pragma-unroll-threshold=1000000"],
-    "corrmfmadpp": ["-DCMF_A_DPP=1"],
 }
 
 
