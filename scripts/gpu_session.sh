@@ -144,13 +144,21 @@ for s in ${STEPS:-smoke tests bench}; do
       L=$PWD/scripts/tune/ab/libsrcdsp_hip_mixmfma.so
       SRCDSP_HIP_LIB=$L step mixlib_check_$TAG 300 python -u scripts/tune/mixdecim_mfma_lib.py
       SRCDSP_HIP_LIB=$L step mixlib_tests_$TAG 900 python -u -m pytest tests -m gpu -q --timeout 120 \
-        --timeout-method thread --maxfail=30 -k "chain or mixdecim or config4 or mixer or pipeline or streams"
+        --timeout-method thread --maxfail=30 -k "chain or mixdecim or config4 or mixer or pipeline or streams or decim"
       for rep in 1 2; do
         sleep ${IDLE:-8}
         step mixlib_benchprod${rep}_$TAG 300 python -u bench.py --workload mixdecim --no-cpu-baseline --no-pcie \
           --warmup 5 --steps 20
         sleep ${IDLE:-8}
         SRCDSP_HIP_LIB=$L step mixlib_bench${rep}_$TAG 300 python -u bench.py --workload mixdecim --no-cpu-baseline \
+          --no-pcie --warmup 5 --steps 20
+      done
+      for rep in 1 2; do  # row a2 (the plain decimator) through the same kernel
+        sleep ${IDLE:-8}
+        step mixlib_a2prod${rep}_$TAG 300 python -u bench.py --workload ci16decim --no-cpu-baseline --no-pcie \
+          --warmup 5 --steps 20
+        sleep ${IDLE:-8}
+        SRCDSP_HIP_LIB=$L step mixlib_a2${rep}_$TAG 300 python -u bench.py --workload ci16decim --no-cpu-baseline \
           --no-pcie --warmup 5 --steps 20
       done
       SRCDSP_HIP_LIB=$L step mixlib_steady_$TAG 300 python -u bench.py --workload mixdecim --no-cpu-baseline --no-pcie \

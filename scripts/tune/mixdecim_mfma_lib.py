@@ -13,7 +13,10 @@ adds to the product's own tests:
 * mixer tables of 4096, 1024 and 64 entries, positive and negative frequency;
 * taps past two int8 limbs (|c| >= 32640) and a 256-tap filter: not eligible,
   the product path serves them (the launch counter must not move);
-* srcdsp_tune_mixdecim_mfma_launches() grows by exactly the eligible calls.
+* srcdsp_tune_mixdecim_mfma_launches() grows by exactly the eligible calls;
+* the plain decimator (row a2, srcdsp_decim_step) through the same kernel
+  without the mixer: the same streams at 1, 31, 127 and 128 taps
+  (srcdsp_tune_decim_mfma_launches()).
 
   SRCDSP_HIP_LIB=scripts/tune/ab/libsrcdsp_hip_mixmfma.so python scripts/tune/mixdecim_mfma_lib.py"""
 import ctypes as C
@@ -65,6 +68,27 @@ def run_case(S, torch, c, N, f, calls, seed, limbs_ok):
     return bad, eligible
 
 
+def run_plain(S, torch, c, calls, seed):
+    """the plain decimator (row a2) stepped through calls, against the oracle's"""
+    o = pyoracle.Oracle(0)
+    od = o.decim(1, 4, c)
+    d = S.FilterDnsamplingFir(c, 4, *TYPES)
+    x = o.gen_ci16(seed, 0, 0, sum(calls), -32768, 32767)
+    bad, pos = [], 0
+    for k, ln in enumerate(calls):
+        xs = x[pos:pos + ln]
+        pos += ln
+        want = od.step(xs)
+        y = torch.empty((ln // 4, 2), dtype=torch.int16, device="cuda")
+        d.step(torch.from_numpy(np.ascontiguousarray(xs)).cuda(), y)
+        got = y.cpu().numpy()
+        if not np.array_equal(got, want):
+            i = int(np.nonzero((got != want).any(axis=1))[0][0])
+            bad.append(f"call {k} (len {ln}): first differing output {i}")
+            break
+    return bad
+
+
 def main():
     import torch
     import srcdsp_amd as S
@@ -95,6 +119,17 @@ def main():
     bad, _ = run_case(S, torch, taps(256, 3000, 5), 4096, 0.1, calls[:3], 30, False)
     res["cases"]["256taps_product_path"] = {"mismatches": bad, "mfma_calls": count() - before}
     ok &= not bad and count() == before
+    # the plain decimator (row a2: srcdsp_decim_step without a mixer) through the same kernel
+    pcount = lib.srcdsp_tune_decim_mfma_launches
+    pcount.restype = C.c_long
+    for name, c in (("plain_127q14", taps(127, None, 0)), ("plain_128taps", taps(128, 20000, 1)),
+                    ("plain_31taps", taps(31, 9000, 2)), ("plain_1tap", np.array([16384], np.int32))):
+        before = pcount()
+        bad = run_plain(S, torch, c, calls, 40 + len(res["cases"]))
+        launched = pcount() - before
+        res["cases"][name] = {"mismatches": bad, "calls": len(calls), "mfma_calls": launched}
+        ok &= not bad and launched == len(calls)
+        print(name, json.dumps(res["cases"][name]), flush=True)
     res["ok"] = bool(ok)
     print(json.dumps({"ok": res["ok"]}))
     out = os.path.join(ROOT, "gpurun_out", "mixdecim_mfma_lib.json")

@@ -17,7 +17,9 @@
 //   (limitScale16 as the product's limit16_pair_sh), any length (the last tile
 //   reads zeros past the end and stores only outputs < n_out);
 // * the tap fragments built on the host per decimator, rebuilt when its taps
-//   change (a side table keyed by the decimator's address and its taps).
+//   change (a side table keyed by the decimator's address and its taps);
+// * the same kernel without the mixer serves the plain complex<int16_t>
+//   decimator's step (row a2, core_step).
 
 namespace mmf {
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -63,6 +65,9 @@ __device__ __forceinline__ v2u mix_words(const int16_t* tab, unsigned ph, unsign
 }
 }  // namespace mmf
 
+// MIX = false: the plain complex<int16_t> decimator (row a2's srcdsp_decim_step):
+// the staged samples are the input itself
+template <bool MIX>
 __global__ void __launch_bounds__(mmf::LANES, 2)
 mixdecim_mfma_step_i8(const uint32_t* __restrict__ x, long n_in, const uint32_t* __restrict__ hist, int H,
                       uint32_t* __restrict__ hist_out, const mmf::v4i* __restrict__ bfrag,
@@ -77,15 +82,17 @@ mixdecim_mfma_step_i8(const uint32_t* __restrict__ x, long n_in, const uint32_t*
     // lane tid's granules g = tid + LANES k start at staged sample 4 g of every
     // tile (global sample tile * 4 TILE - HALO + 4 g); N | 4 TILE, so their
     // phases are the same in every tile (mod 2^32 arithmetic: N is a power of 2)
-    v2u tw[NG][4];
+    v2u tw[MIX ? NG : 1][4];
+    if constexpr (MIX) {
 #pragma unroll
-    for (int k = 0; k < NG; ++k) {
-        const int g = tid + LANES * k;
-        uint32_t ph = (phi0 + (uint32_t)(4 * g - HALO) * freq) & (N - 1);
+        for (int k = 0; k < NG; ++k) {
+            const int g = tid + LANES * k;
+            uint32_t ph = (phi0 + (uint32_t)(4 * g - HALO) * freq) & (N - 1);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            tw[k][q] = mix_words(tab, ph, N);
-            ph = (ph + freq) & (N - 1);
+            for (int q = 0; q < 4; ++q) {
+                tw[k][q] = mix_words(tab, ph, N);
+                ph = (ph + freq) & (N - 1);
+            }
         }
     }
     v4i B[6];
@@ -113,9 +120,11 @@ mixdecim_mfma_step_i8(const uint32_t* __restrict__ x, long n_in, const uint32_t*
             const long idx = n_in - H + k;
             uint32_t wv;
             if (idx >= 0) {
-                const v2u t = mix_words(tab, (phi0 + (uint32_t)idx * freq) & (N - 1), N);
-                const uint32_t xq = x[idx];
-                wv = pack_clamp_sh(sdot2w(xq, t[0]), sdot2w(xq, t[1]), 14u);
+                wv = x[idx];
+                if constexpr (MIX) {
+                    const v2u t = mix_words(tab, (phi0 + (uint32_t)idx * freq) & (N - 1), N);
+                    wv = pack_clamp_sh(sdot2w(wv, t[0]), sdot2w(wv, t[1]), 14u);
+                }
             } else {
                 wv = hist[H + idx];
             }
@@ -137,9 +146,12 @@ mixdecim_mfma_step_i8(const uint32_t* __restrict__ x, long n_in, const uint32_t*
             uint32_t m[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const v2u t = tw[k][q];
-                const uint32_t xq = v[q];
-                m[q] = pack_clamp_sh(sdot2w(xq, t[0]), sdot2w(xq, t[1]), 14u);
+                if constexpr (MIX) {
+                    const v2u t = tw[k][q];
+                    m[q] = pack_clamp_sh(sdot2w(v[q], t[0]), sdot2w(v[q], t[1]), 14u);
+                } else {
+                    m[q] = v[q];
+                }
             }
             const uint32_t t0 = __builtin_amdgcn_perm(m[1], m[0], 0x05010400u);
             const uint32_t t1 = __builtin_amdgcn_perm(m[3], m[2], 0x05010400u);
@@ -248,23 +260,38 @@ static int mixmfma_prepare(FirCore& f, MixMfmaTaps& e)
     return SRCDSP_OK;
 }
 
-static long g_mixmfma_launches = 0;  // calls that took the matrix-core path (the check script reads it)
+static long g_mixmfma_launches = 0;  // calls that took the matrix-core path (the check scripts read them)
+static long g_decmfma_launches = 0;
 
 extern "C" __attribute__((visibility("default"))) long srcdsp_tune_mixdecim_mfma_launches() { return g_mixmfma_launches; }
+extern "C" __attribute__((visibility("default"))) long srcdsp_tune_decim_mfma_launches() { return g_decmfma_launches; }
+
+static bool decmfma_usable(FirCore& f, const void* d_in, size_t n_in, const void* d_out)
+{
+    const unsigned sh = f.shift() & 31u;
+    return f.kv == KV_CI16_I32 && f.M == 4 && f.ntaps >= 1 && f.ntaps <= mmf::MAX_TAPS && sh != 0 &&
+           n_in % 4 == 0 && 4 * n_in < (1ul << 31) && ((uintptr_t)d_in & 15) == 0 && ((uintptr_t)d_out & 15) == 0;
+}
 
 static bool mixmfma_usable(FirCore& f, const MixerState& m, const void* d_in, size_t n_in, const void* d_out)
 {
     const char* off = getenv("SRCDSP_MIXDECIM_MFMA");
     if (off && off[0] == '0') return false;
-    const unsigned sh = f.shift() & 31u;
-    return f.kv == KV_CI16_I32 && f.M == 4 && f.ntaps >= 1 && f.ntaps <= mmf::MAX_TAPS && sh != 0 &&
-           m.N >= 4 && m.N <= 4096 && (m.N & (m.N - 1)) == 0 && n_in % 4 == 0 && 4 * n_in < (1ul << 31) &&
-           ((uintptr_t)d_in & 15) == 0 && ((uintptr_t)d_out & 15) == 0;
+    return decmfma_usable(f, d_in, n_in, d_out) && m.N >= 4 && m.N <= 4096 && (m.N & (m.N - 1)) == 0;
+}
+
+// the plain decimator (core_step without a mixer); SRCDSP_DECIM_MFMA=0: off
+static bool plainmfma_usable(FirCore& f, const void* d_in, size_t n_in, const void* d_out)
+{
+    const char* off = getenv("SRCDSP_DECIM_MFMA");
+    if (off && off[0] == '0') return false;
+    return decmfma_usable(f, d_in, n_in, d_out);
 }
 
 // core_step's contract (ordering, history double buffer) with the matrix-core kernel;
 // SRCDSP_ERR_UNSUPPORTED when the taps do not fit two limbs (the caller then takes core_step)
-static int mixmfma_step(FirCore& f, const MixerState& m, const void* d_in, size_t n_in, void* d_out, hipStream_t s)
+template <bool MIX>
+static int mfma_decim_step(FirCore& f, const MixerState* m, const void* d_in, size_t n_in, void* d_out, hipStream_t s)
 {
     MixMfmaTaps& e = mixmfma_taps(f);
     int rc = mixmfma_prepare(f, e);
@@ -272,7 +299,7 @@ static int mixmfma_step(FirCore& f, const MixerState& m, const void* d_in, size_
     if (!e.ok) return SRCDSP_ERR_UNSUPPORTED;
     static bool attr = false;
     if (!attr) {
-        SRCDSP_HIP_TRY(hipFuncSetAttribute((const void*)mixdecim_mfma_step_i8,
+        SRCDSP_HIP_TRY(hipFuncSetAttribute((const void*)mixdecim_mfma_step_i8<MIX>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, mmf::LDS_TOTAL));
         attr = true;
     }
@@ -280,15 +307,20 @@ static int mixmfma_step(FirCore& f, const MixerState& m, const void* d_in, size_
     if (rc) return rc;
     const long n = (long)n_in;
     const long n_tiles = (n + 4 * mmf::TILE - 1) / (4 * mmf::TILE);
-    const uint32_t phi0 = (uint32_t)(int32_t)m.phi, fr = (uint32_t)(int32_t)m.freq;
+    const uint32_t phi0 = MIX ? (uint32_t)(int32_t)m->phi : 0u, fr = MIX ? (uint32_t)(int32_t)m->freq : 0u;
     const int H = f.ntaps - 1;
     const int grid = (int)std::min<long>(512, n_tiles);
-    ++g_mixmfma_launches;
-    hipLaunchKernelGGL(mixdecim_mfma_step_i8, dim3(grid), dim3(mmf::LANES), mmf::LDS_TOTAL, s, (const uint32_t*)d_in,
+    ++(MIX ? g_mixmfma_launches : g_decmfma_launches);
+    hipLaunchKernelGGL(mixdecim_mfma_step_i8<MIX>, dim3(grid), dim3(mmf::LANES), mmf::LDS_TOTAL, s, (const uint32_t*)d_in,
                        n, (const uint32_t*)f.d_hist[f.cur], H, (uint32_t*)f.d_hist[f.cur ^ 1],
-                       (const mmf::v4i*)e.d_frag, (const int16_t*)m.d_table,
-                       m.N, phi0, fr, e.bias, f.shift() & 31u, (uint32_t*)d_out, n_tiles);
+                       (const mmf::v4i*)e.d_frag, MIX ? (const int16_t*)m->d_table : nullptr,
+                       MIX ? m->N : 1u, phi0, fr, e.bias, f.shift() & 31u, (uint32_t*)d_out, n_tiles);
     SRCDSP_HIP_TRY(hipGetLastError());
     f.cur ^= 1;
     return f.order.after(s);
+}
+
+static int mixmfma_step(FirCore& f, const MixerState& m, const void* d_in, size_t n_in, void* d_out, hipStream_t s)
+{
+    return mfma_decim_step<true>(f, &m, d_in, n_in, d_out, s);
 }

@@ -165,8 +165,21 @@ STALE = {"r4mix": "round 6 moved config 4's mixer table into registers (ccc91a7)
 # config 4's mixer -> decimator chain with the tap loop on the i8 matrix cores
 # (scripts/tune/mixdecim_mfma_step.h)
 PATCHES["mixmfma"] = [
-    ("decim.hip", "}  // namespace srcdsp\n\nusing namespace srcdsp;\n",
-     "#include \"mixdecim_mfma_step.h\"\n\n}  // namespace srcdsp\n\nusing namespace srcdsp;\n"),
+    ("decim.hip", "static int core_step(FirCore &f, const void *d_in, size_t n_in, void *d_out, size_t n_out, hipStream_t s,\n"
+                  "                     const MixerState *mix) {\n"
+                  "    SRCDSP_ARG_CHECK(n_out * f.M == n_in, \"step: output size * M must equal input size\");\n"
+                  "    if (n_in == 0) return SRCDSP_OK;\n"
+                  "    SRCDSP_ARG_CHECK(d_in && d_out, \"step: null buffer\");\n",
+     "#include \"mixdecim_mfma_step.h\"\n\n"
+     "static int core_step(FirCore &f, const void *d_in, size_t n_in, void *d_out, size_t n_out, hipStream_t s,\n"
+     "                     const MixerState *mix) {\n"
+     "    SRCDSP_ARG_CHECK(n_out * f.M == n_in, \"step: output size * M must equal input size\");\n"
+     "    if (n_in == 0) return SRCDSP_OK;\n"
+     "    SRCDSP_ARG_CHECK(d_in && d_out, \"step: null buffer\");\n"
+     "    if (!mix && plainmfma_usable(f, d_in, n_in, d_out)) {  // tuning variant: row a2 on the matrix cores\n"
+     "        const int r = mfma_decim_step<false>(f, nullptr, d_in, n_in, d_out, s);\n"
+     "        if (r != SRCDSP_ERR_UNSUPPORTED) return r;\n"
+     "    }\n"),
     ("decim.hip", "    rc = core_step(f, d_in, n_in, d_out, n_out, s, &m);\n",
      "    rc = mixmfma_usable(f, m, d_in, n_in, d_out) ? mixmfma_step(f, m, d_in, n_in, d_out, s)\n"
      "                                                 : SRCDSP_ERR_UNSUPPORTED;\n"
