@@ -166,6 +166,20 @@ def test_bench_main_two_ranks_end_to_end_on_host():
 
 
 @pytest.mark.skipif(not os.path.exists(DIGESTS), reason="tests/golden/channel_digests.json not generated")
+def test_bench_main_eight_ranks_end_to_end_on_host():
+    """The driver's N = 8 command on the CPU (8 gloo ranks, host stand-ins):
+    configs[2] itself (64 channels, 8 per rank) with every rank's digests and
+    all 64 gathered at rank 0 clean, the main series one channel per rank."""
+    line = _host_ranks(8)
+    assert line["n_gpus"] == 8 and line["world_size_reported"] == 8
+    assert (line["parity"]["channels_checked"], line["parity"]["mismatches"]) == (8, 0)
+    sh = line["configs2_share"]
+    assert sh["channels_total"] == 64 and sh["baseline_config"] == "configs[2]"
+    assert (sh["parity"]["channels_checked"], sh["parity"]["mismatches"]) == (64, 0)
+    assert (sh["gather_parity"]["channels_checked"], sh["gather_parity"]["mismatches"]) == (64, 0)
+
+
+@pytest.mark.skipif(not os.path.exists(DIGESTS), reason="tests/golden/channel_digests.json not generated")
 def test_bench_parity_reports_a_corrupted_channel():
     """One flipped input sample on channel 9 (rank 1's share, not rank 0's):
     the summed counts over ranks and the gathered check both show exactly one
